@@ -1,0 +1,74 @@
+// tests/native/glibc_math_check.cpp -- exhaustive host check that
+// se-195-project-ray-tracer_amd/csrc/rt_glibc_math.h reproduces the host
+// glibc's float libm bit for bit over the hot path's input domains.
+// Prints one "name checked mismatches first_bad_input" line per domain.
+#include <math.h>
+#include <stdio.h>
+#include <stdint.h>
+#include <string.h>
+#include "rt_glibc_math.h"
+
+static inline bool same(float a, float b)
+{
+    if (a != a && b != b) return true;
+    return rtm::f2u(a) == rtm::f2u(b);
+}
+
+template <class F, class G>
+static void run(const char *name, uint64_t lo, uint64_t hi, F ours, G ref)
+{
+    unsigned long long bad = 0, first = ~0ull;
+#pragma omp parallel for schedule(static, 1 << 16) reduction(+ : bad) reduction(min : first)
+    for (uint64_t u = lo; u <= hi; u++) {
+        float x = rtm::u2f((uint32_t)u);
+        if (!same(ours(x), ref(x))) { bad++; if (u < first) first = u; }
+    }
+    printf("%s %llu %llu 0x%08llx\n", name, (unsigned long long)(hi - lo + 1), bad,
+           first == ~0ull ? 0ull : first);
+    fflush(stdout);
+}
+
+int main(int argc, char **argv)
+{
+    const float g = 1.f / 2.2f;
+    bool quick = argc > 1 && !strcmp(argv[1], "quick");
+    uint32_t step_hi = quick ? 0x3c000000u : 0x40000000u;
+    // powf(dot, 20): raytracer.cpp:165, dot in (0, ~1]
+    run("powf_y20", 0, step_hi, [](float x) { return rtm::powf(x, 20.0f); },
+        [](float x) { return ::powf(x, 20.0f); });
+    // toInt gamma: vec.h:62, x in [0, 1] (and -0)
+    run("powf_gamma", 0, 0x3f800000u, [g](float x) { return rtm::powf(x, g); },
+        [g](float x) { return ::powf(x, g); });
+    run("powf_gamma_negzero", 0x80000000u, 0x80000000u, [g](float x) { return rtm::powf(x, g); },
+        [g](float x) { return ::powf(x, g); });
+    // expf(absorbance <= 0): raytracer.cpp:487-489 -- every float
+    run("expf_neg", 0x80000000u, quick ? 0xa0000000u : 0xffffffffu, [](float x) { return rtm::expf(x); },
+        [](float x) { return ::expf(x); });
+    run("expf_pos", 0, quick ? 0x20000000u : 0x7fffffffu, [](float x) { return rtm::expf(x); },
+        [](float x) { return ::expf(x); });
+    // sinf/cosf(2*PI*u): geomfunc.h:65-66,261-262 -- every float in [-8, 8]
+    uint32_t trig_hi = quick ? 0x3d000000u : 0x41000000u;
+    run("sinf_pos", 0, trig_hi, [](float x) { return rtm::sinf(x); }, [](float x) { return ::sinf(x); });
+    run("cosf_pos", 0, trig_hi, [](float x) { return rtm::cosf(x); }, [](float x) { return ::cosf(x); });
+    run("sinf_neg", 0x80000000u, 0x80000000u + trig_hi, [](float x) { return rtm::sinf(x); },
+        [](float x) { return ::sinf(x); });
+    run("cosf_neg", 0x80000000u, 0x80000000u + trig_hi, [](float x) { return rtm::cosf(x); },
+        [](float x) { return ::cosf(x); });
+    run("sincosf_sin", 0, trig_hi, [](float x) { return rtm::sinf(x); },
+        [](float x) { float s, c; ::sincosf(x, &s, &c); return s; });
+    run("sincosf_cos", 0, trig_hi, [](float x) { return rtm::cosf(x); },
+        [](float x) { float s, c; ::sincosf(x, &s, &c); return c; });
+    // The exact smallpt domain: r1 = (2*PI) * (m * 2^-23), m < 2^23.
+    {
+        unsigned long long bad = 0;
+        const float twopi = 2.f * 3.14159265358979323846f;
+#pragma omp parallel for reduction(+ : bad)
+        for (uint32_t m = 0; m < (1u << 23); m++) {
+            float u = (float)m * 0x1p-23f;
+            float r = twopi * u;
+            if (!same(rtm::sinf(r), ::sinf(r)) || !same(rtm::cosf(r), ::cosf(r))) bad++;
+        }
+        printf("trig_smallpt_domain %u %llu 0x0\n", 1u << 23, bad);
+    }
+    return 0;
+}

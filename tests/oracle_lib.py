@@ -1,0 +1,156 @@
+"""ctypes bindings for oracle/liboracle.so and oracle/_ref/*.so.
+
+TEST INFRASTRUCTURE ONLY: the oracle is the parity checker and the CPU
+baseline; nothing in se-195-project-ray-tracer_amd/ imports this module.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+
+
+class V3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class Primitive(C.Structure):  # raytracer.h:23-32, 96 B
+    _fields_ = [("type", C.c_int32), ("m_Light", C.c_int32), ("m_Centre", V3),
+                ("m_SqRadius", C.c_float), ("m_Radius", C.c_float), ("m_RRadius", C.c_float),
+                ("plane_N", V3), ("plane_D", C.c_float), ("plane_cell", C.c_float * 4),
+                ("m_Color", V3), ("m_Refl", C.c_float), ("m_Refr", C.c_float),
+                ("m_Diff", C.c_float), ("m_Spec", C.c_float), ("m_RIndex", C.c_float)]
+
+
+class Sphere(C.Structure):  # geom.h:43-47, 44 B
+    _fields_ = [("rad", C.c_float), ("p", V3), ("e", V3), ("c", V3), ("refl", C.c_int32)]
+
+
+class Camera(C.Structure):  # camera.h:29-34, 60 B
+    _fields_ = [("orig", V3), ("target", V3), ("dir", V3), ("x", V3), ("y", V3)]
+
+
+assert C.sizeof(Primitive) == 96 and C.sizeof(Sphere) == 44 and C.sizeof(Camera) == 60
+
+_u64p = C.POINTER(C.c_uint64)
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(ORACLE_DIR, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.orw_scene_init.argtypes = [C.POINTER(Primitive), C.c_int]
+        L.orw_render.argtypes = [C.POINTER(Primitive), C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                 C.c_int, C.c_int, _u64p, C.c_int]
+        L.orw_primitive_intersect.argtypes = [C.POINTER(Primitive), C.c_void_p, C.POINTER(C.c_float)]
+        L.orw_primitive_normal.argtypes = [C.POINTER(Primitive), C.c_void_p, C.c_void_p]
+        L.ors_cornell.argtypes = [C.POINTER(Sphere), C.c_int]
+        L.ors_update_camera.argtypes = [C.POINTER(Camera), C.c_int, C.c_int]
+        L.ors_seeds_init.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
+        L.ors_get_random.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.ors_get_random.restype = C.c_float
+        L.ors_render.argtypes = [C.POINTER(Sphere), C.c_uint, C.POINTER(Camera), C.c_void_p,
+                                 C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 C.c_int, C.c_int, C.c_int, _u64p, C.c_int]
+        L.ors_hypersphere.argtypes = [C.POINTER(Sphere), C.c_int, C.c_double]
+        L.or_fnv1a64.argtypes = [C.c_void_p, C.c_size_t]
+        L.or_fnv1a64.restype = C.c_uint64
+        _lib = L
+    return _lib
+
+
+def fnv1a64(arr):
+    a = np.ascontiguousarray(arr)
+    return "%016x" % lib().or_fnv1a64(a.ctypes.data, a.nbytes)
+
+
+# ---------------------------------------------------------------- Whitted
+def whitted_scene():
+    prims = (Primitive * 50)()
+    n = lib().orw_scene_init(prims, 50)
+    return prims, n
+
+
+def whitted_render(w, h, row_begin=20, row_end=None, nthreads=1, prims=None, n=None):
+    """Engine_InitRender + Engine_Render on a zero-cleared frame; returns
+    (uint32 frame[h,w], counters[4])."""
+    if prims is None:
+        prims, n = whitted_scene()
+    if row_end is None:
+        row_end = h - 70
+    frame = np.zeros((h, w), dtype=np.uint32)
+    cnt = (C.c_uint64 * 4)()
+    lib().orw_render(prims, n, frame.ctypes.data, w, h, row_begin, row_end, cnt, nthreads)
+    return frame, list(cnt)
+
+
+# ---------------------------------------------------------------- smallpt
+def cornell():
+    s = (Sphere * 9)()
+    n = lib().ors_cornell(s, 9)
+    return s, n
+
+
+def cornell_camera(w, h):
+    """mainCPU camera (smallptCPU.cpp:184-185) + UpdateCamera."""
+    cam = Camera()
+    cam.orig = V3(50.0, 45.0, 205.6)
+    cam.target = V3(50.0, np.float32(45) - np.float32(0.042612), 204.6)
+    lib().ors_update_camera(C.byref(cam), w, h)
+    return cam
+
+
+def seeds(w, h, seed=1):
+    s = np.zeros(2 * w * h, dtype=np.uint32)
+    lib().ors_seeds_init(s.ctypes.data, s.size, seed)
+    return s
+
+
+def smallpt_render(spheres, n, cam, colors, seeds_arr, pixels, w, h, first_sample, nsamples,
+                   row_begin=0, row_end=None, dl=0, nthreads=1):
+    if row_end is None:
+        row_end = h
+    cnt = (C.c_uint64 * 4)()
+    lib().ors_render(spheres, n, C.byref(cam), colors.ctypes.data, seeds_arr.ctypes.data,
+                     pixels.ctypes.data, w, h, row_begin, row_end, first_sample, nsamples, dl,
+                     cnt, nthreads)
+    return list(cnt)
+
+
+def hypersphere(max_depth, cap):
+    buf = (Sphere * cap)()
+    total = lib().ors_hypersphere(buf, cap, float(max_depth))
+    return buf, total
+
+
+# ---------------------------------------------------------------- _ref
+def ref_libs():
+    """(whitted_scene_lib, smallpt_lib) built from /root/reference, or None."""
+    d = os.path.join(ORACLE_DIR, "_ref")
+    w = os.path.join(d, "libref_whitted_scene.so")
+    s = os.path.join(d, "libref_smallpt.so")
+    if not (os.path.exists(w) and os.path.exists(s)):
+        return None
+    W = C.CDLL(w)
+    W.ref_whitted_scene.argtypes = [C.POINTER(Primitive), C.c_int]
+    W.ref_primitive_intersect.argtypes = [C.POINTER(Primitive), C.c_void_p, C.POINTER(C.c_float)]
+    W.ref_primitive_normal.argtypes = [C.POINTER(Primitive), C.c_void_p, C.c_void_p]
+    S = C.CDLL(s)
+    S.ref_cornell.argtypes = [C.POINTER(Sphere), C.c_int]
+    S.ref_get_random.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    S.ref_get_random.restype = C.c_float
+    S.ref_smallpt_render.argtypes = [C.POINTER(Sphere), C.c_uint, C.POINTER(Camera), C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.c_int, C.c_int, C.c_int]
+    return W, S
