@@ -1,0 +1,257 @@
+"""bench.py -- headline benchmark of the MI355X ray-trace hot path.
+
+Workload (BASELINE.json metric "Mrays/sec + ms/frame @1920x1080 Cornell-64spp,
+1/2/4/8 GPU; % HBM roofline"): one step = one 1920x1080 frame of the smallpt
+Cornell scene (smallptgpu-v1.6/scene.h:29-40, reference camera) at 64
+samples per pixel from the initial state (currentSample 0, AllocateBuffers'
+glibc rand() seeds) -- RadiancePathTracing for every sample of every pixel,
+running average, toInt pack -- plus, for N > 1, the RCCL all-gather that
+assembles the HDR accumulator and the RGBA8 frame on every rank.
+
+Rows are sharded over ranks in equal contiguous bands (strong scaling: the
+frame is fixed, each of N GPUs renders 1/N of it).  Rays = Intersect +
+IntersectP calls, counted by the kernel itself.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-whitted]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "se-195-project-ray-tracer_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (torch first: one HIP runtime in the process)
+import torch.distributed as dist  # noqa: E402
+
+import rtamd  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: peak FP32 vector
+W, H, SPP = 1920, 1080, 64
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-whitted", action="store_true", help="skip the Whitted side line")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU sample length")
+    return ap.parse_args()
+
+
+def band(rank, world):
+    """Contiguous row band [r0, r1) of rank `rank` (flipped-slot order so
+    the colour slots of rank k are the k-th contiguous chunk)."""
+    B = H // world
+    assert B * world == H, "H must divide by the GPU count"
+    r0 = H - (rank + 1) * B
+    return r0, r0 + B
+
+
+def cpu_baseline(args):
+    """Oracle (C restatement, OpenMP over rows) on a bounded band of the same
+    workload: rows of the 1920x1080 Cornell frame at 64 spp, sized to about
+    args.cpu_seconds of host time."""
+    import oracle_lib as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    S, n = O.cornell()
+    cam = O.cornell_camera(W, H)
+    col = np.zeros(3 * W * H, np.float32)
+    px = np.zeros(W * H, np.uint32)
+    seeds = O.seeds(W, H)
+    # calibration band
+    rows = max(threads, 8)
+    r0 = H // 2 - rows // 2
+    t0 = time.perf_counter()
+    c = O.smallpt_render(S, n, cam, col, seeds.copy(), px, W, H, 0, SPP, row_begin=r0,
+                         row_end=r0 + rows, nthreads=threads)
+    dt = time.perf_counter() - t0
+    rows2 = int(min(H, max(rows, rows * args.cpu_seconds / max(dt, 1e-3))))
+    r0 = max(0, H // 2 - rows2 // 2)
+    t0 = time.perf_counter()
+    c = O.smallpt_render(S, n, cam, col, seeds.copy(), px, W, H, 0, SPP, row_begin=r0,
+                         row_end=r0 + rows2, nthreads=threads)
+    dt = time.perf_counter() - t0
+    rays = c[0] + c[1]
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": "oracle/smallpt_oracle.c, rows [%d,%d) of the 1920x1080 Cornell frame at 64 spp "
+                      "(%d samples, %.1f s, %d threads; %.3f Msamples/s)"
+                      % (r0, r0 + rows2, c[3], dt, threads, c[3] / dt / 1e6)}
+
+
+def whitted_line(args, dev):
+    """Side line: BASELINE configs[1], Whitted 1920x1080 one frame on 1 GPU
+    (device-resident frame, kernel timed with HIP events)."""
+    prims, n = rtamd.scenes.whitted_scene()
+    d_prims = torch.frombuffer(bytearray(bytes(prims)), dtype=torch.uint8).to(dev)
+    frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev)
+    L = rtamd.lib()
+
+    def run(c):
+        rtamd.check(L.rtw_render_async(d_prims.data_ptr(), n, frame.data_ptr(), W, H, 20, H - 70,
+                                       c.data_ptr() if c is not None else None, s.cuda_stream))
+
+    run(cnt)
+    torch.cuda.synchronize(dev)
+    counts = cnt.tolist()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    e0.record(s)
+    for _ in range(reps):
+        run(None)
+    e1.record(s)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    rays = counts[0] + counts[1]
+    out = {"workload": "Whitted raytracer3.0.06 scene 1920x1080, 9 primary rays/px, rows [20,1010)",
+           "ms_per_frame": round(ms, 4), "Mrays_per_s": round(rays / ms / 1e3, 2),
+           "rays_per_frame": rays, "ray_prim_tests": counts[2]}
+    if not args.no_cpu:
+        import oracle_lib as O
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        t0 = time.perf_counter()
+        _, c = O.whitted_render(W, H, row_begin=20, row_end=H - 70, nthreads=threads)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round((c[0] + c[1]) / dt / 1e6, 3), "unit": "Mrays/s",
+                               "cores": threads, "kind": "port", "ms_per_frame": round(dt * 1e3, 1),
+                               "sample": "oracle/whitted_oracle.c, the full frame"}
+    return out
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    distributed = world > 1
+    if distributed:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    rtamd.set_device(local)
+    L = rtamd.lib()
+
+    spheres, ns = rtamd.scenes.cornell()
+    cam = rtamd.scenes.cornell_camera(W, H)
+    d_spheres = torch.frombuffer(bytearray(bytes(spheres)), dtype=torch.uint8).to(dev)
+    seeds0 = torch.from_numpy(rtamd.scenes.seeds(W, H).view(np.int32)).to(dev)  # pristine
+    seeds = torch.empty_like(seeds0)
+    colors = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
+    pixels = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+    r0, r1 = band(rank, world)
+    B = r1 - r0
+    s = torch.cuda.current_stream(dev)
+    if distributed:
+        col_parts = list(colors.view(world, 3 * B * W).unbind(0))       # flipped slots: rank k = chunk k
+        px_parts = [pixels[(H - (k + 1) * B) * W:(H - k * B) * W] for k in range(world)]
+        my_col = colors[(H - r1) * W * 3:(H - r0) * W * 3]
+        my_px = pixels[r0 * W:r1 * W]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+
+    def step(i=None, counters=None):
+        if i is not None:
+            ev[i][0].record(s)
+        rtamd.check(L.spt_render_async(d_spheres.data_ptr(), ns, C.byref(cam), colors.data_ptr(),
+                                       seeds0.data_ptr(), seeds.data_ptr(), pixels.data_ptr(), W, H, r0, r1,
+                                       0, SPP, rtamd.SPT_PATH_TRACING,
+                                       counters.data_ptr() if counters is not None else None,
+                                       s.cuda_stream))
+        if i is not None:
+            ev[i][1].record(s)
+        if distributed:
+            dist.all_gather(col_parts, my_col.clone())
+            dist.all_gather(px_parts, my_px.clone())
+
+    for _ in range(args.warmup):
+        step()
+    cnt.zero_()
+    step(counters=cnt)                      # one counted frame (counts are deterministic)
+    torch.cuda.synchronize(dev)
+    counts = cnt.clone()
+    if distributed:
+        dist.all_reduce(counts)
+    counts = counts.tolist()
+    rays_per_frame = counts[0] + counts[1]
+
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if distributed:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = t.tolist()
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # Roofline: algorithmic HBM bytes of one launch =
+    # 32 B per pixel of the band (seeds 8 in + 8 out, colour 12 out, pixel 4
+    # out) + the scene (44 B per sphere).  The kernel is VALU-bound; the FP32
+    # view counts 20 FLOP per ray-sphere test.
+    launch_bytes = 32 * B * W + 44 * ns
+    achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
+    flops = 20.0 * counts[2] / world
+    out = {
+        "metric": "Mrays/sec + ms/frame @1920x1080 Cornell-64spp, 1/2/4/8 GPU; % HBM roofline",
+        "value": round(rays_per_frame / (ms_per_step * 1e-3) / 1e6, 2),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: reference Cornell scene (scene.h:29-40), glibc rand() seeds, random-free camera",
+        "config": {"workload": "smallpt Cornell 1920x1080 64spp RadiancePathTracing, one frame per step",
+                   "frame": [W, H], "spp": SPP, "spheres": ns, "rows_per_gpu": B,
+                   "parallelism": "row bands x%d + RCCL all-gather" % world if world > 1 else "single GPU"},
+        "frames_per_s": round(1e3 / ms_per_step, 3),
+        "Msamples_per_s": round(W * H * SPP / (ms_per_step * 1e-3) / 1e6, 2),
+        "rays_per_frame": rays_per_frame,
+        "kernel_ms": round(kern_ms, 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "note": "compute-bound kernel: HBM roofline reported because the metric asks; "
+                             "see valu"},
+        "valu": {"achieved_tflops": round(flops / (kern_ms * 1e-3) / 1e12, 3),
+                 "peak_tflops": FP32_PEAK_TFLOPS,
+                 "frac": flops / (kern_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                 "basis": "20 FLOP per ray-sphere test"},
+    }
+    if rank == 0 and world == 1:
+        if not args.no_whitted:
+            out["whitted"] = whitted_line(args, dev)
+        out["cpu_baseline"] = None if args.no_cpu else cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

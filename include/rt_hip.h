@@ -1,0 +1,125 @@
+/*
+ * rt_hip.h -- C-ABI of the MI355X (gfx950) per-pixel ray-trace hot path.
+ *
+ * Drop-in device path for the two reference renderers of
+ * markrosoft/se-195-project-ray-tracer:
+ *
+ *   Whitted (raytracer3.0.06.no_rec.samp): rtw_* replace the OpenCL device
+ *     path of openCLcode.cpp -- AllocateBuffers (:64-120), SetKernelArguments
+ *     (:562-624), ExecuteKernel / clEnqueueNDRangeKernel (:537-560) and
+ *     ReadKernelBuffer (:626-643) -- and compute what the CPU path
+ *     Engine_Render (raytracer.cpp:301-530) computes, bit for bit.
+ *   smallpt (smallptgpu-v1.6): spt_* replace ExecuteKernel (smallptGPU.cpp:617-640)
+ *     and the buffer traffic of UpdateRenderingGPU (:642-782) / ReInit*GPU
+ *     (:784-830), computing UpdateRenderingCPU's per-pixel result
+ *     (smallptCPU.cpp:84-123: flipped colour/seed slot, running average, toInt).
+ *
+ * Plain pointers and sizes only.  Every entry point returns RT_OK (0) or a
+ * negative RT_ERR_* code; rt_last_error() describes the last failure of the
+ * calling thread.  Struct layouts are byte-identical to the reference's.
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_OK 0
+#define RT_ERR_INVALID -1   /* bad argument (null pointer, size, row range) */
+#define RT_ERR_HIP -2       /* HIP runtime failure (rt_last_error has the text) */
+#define RT_ERR_NODEVICE -3  /* no gfx950 device visible */
+
+typedef struct { float x, y, z; } rt_vec3;
+
+/* raytracer.h:23-32 (Material :18-21, plane common.h:49-53) -- 96 bytes */
+typedef struct {
+    int32_t type;                 /* SPHERE = 1, PLANE = 2, BOX = 3 */
+    int32_t m_Light;
+    rt_vec3 m_Centre;
+    float m_SqRadius, m_Radius, m_RRadius;
+    rt_vec3 plane_N;
+    float plane_D;
+    float plane_cell[4];
+    rt_vec3 m_Color;
+    float m_Refl, m_Refr, m_Diff, m_Spec, m_RIndex;
+} rt_primitive;
+
+/* smallptgpu-v1.6/geom.h:43-47 -- 44 bytes */
+typedef struct {
+    float rad;
+    rt_vec3 p, e, c;
+    int32_t refl;                 /* DIFF = 0, SPEC = 1, REFR = 2 */
+} rt_sphere;
+
+/* smallptgpu-v1.6/camera.h:29-34 -- 60 bytes */
+typedef struct {
+    rt_vec3 orig, target;
+    rt_vec3 dir, x, y;
+} rt_camera;
+
+/* ------------------------------------------------------------ runtime */
+const char *rt_last_error(void);
+int rt_device_count(void);
+/* Select the HIP device used by the calling thread's subsequent calls. */
+int rt_set_device(int device);
+/* Release the per-device buffers the blocking entry points cache. */
+int rt_release(void);
+/* Bytes of device memory the blocking entry points currently cache. */
+size_t rt_cached_bytes(void);
+
+/* ------------------------------------------------------------ Whitted */
+/* Blocking, host buffers.  Renders rows [row_begin,row_end) of the w x h
+ * frame into xrgb (uint32 0x00RRGGBB, row-major), leaving other rows
+ * untouched; the reference window is [20, h-70) (raytracer.cpp:281,307).
+ * Requires 20 <= row_begin < row_end <= h (m_SY's recurrence starts at row 20).
+ * counters (nullable, host, 4 x u64): traced rays, shadow rays,
+ * Primitive_Intersect calls, total-internal-reflection events -- the same
+ * quantities oracle/orw_render counts. */
+int rtw_render(const rt_primitive *prims, int nprims, uint32_t *xrgb, int w, int h,
+               int row_begin, int row_end, uint64_t *counters);
+
+/* Asynchronous, device-resident.  d_prims: device copy of the primitive
+ * array; d_xrgb: device frame (w*h); d_counters: device u64[4] accumulated
+ * into (nullable); stream: hipStream_t (NULL = default stream). */
+int rtw_render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int w, int h,
+                     int row_begin, int row_end, uint64_t *d_counters, void *stream);
+
+/* ------------------------------------------------------------ smallpt */
+#define SPT_PATH_TRACING 0       /* RadiancePathTracing    geomfunc.h:167-338 */
+#define SPT_DIRECT_LIGHTING 1    /* RadianceDirectLighting geomfunc.h:340-483 */
+
+/* Blocking, host buffers, whole frame.  Runs samples first_sample ..
+ * first_sample+nsamples-1 of every pixel, exactly as nsamples successive
+ * UpdateRenderingCPU passes with currentSample = first_sample, ...:
+ *   colors  float[3*w*h]  Vec per pixel, slot (h-y-1)*w+x      (in/out)
+ *   seeds   uint32[2*w*h] two MWC words per slot (h-y-1)*w+x    (in/out)
+ *   pixels  uint32[w*h]   toInt(r) | toInt(g)<<8 | toInt(b)<<16 at y*w+x (out)
+ * mode: SPT_PATH_TRACING or SPT_DIRECT_LIGHTING.  counters (nullable,
+ * host, 4 x u64): Intersect calls, IntersectP calls, sphere tests, samples. */
+int spt_render(const rt_sphere *spheres, unsigned nspheres, const rt_camera *camera,
+               float *colors, uint32_t *seeds, uint32_t *pixels, int w, int h,
+               int first_sample, int nsamples, int mode, uint64_t *counters);
+
+/* Asynchronous, device-resident, rows [row_begin,row_end) of the frame.
+ * Buffers are full-frame device arrays laid out as above; seeds are read
+ * from d_seeds_in and the advanced state written to d_seeds_out (may alias).
+ * camera is read on the host at call time (passed by value to the kernel). */
+int spt_render_async(const rt_sphere *d_spheres, unsigned nspheres, const rt_camera *camera,
+                     float *d_colors, const uint32_t *d_seeds_in, uint32_t *d_seeds_out,
+                     uint32_t *d_pixels, int w, int h, int row_begin, int row_end,
+                     int first_sample, int nsamples, int mode, uint64_t *d_counters,
+                     void *stream);
+
+/* Host helper: AllocateBuffers' seed fill (smallptGPU.cpp:105-110) --
+ * srand(seed); seeds[i] = max(rand(), 2) for i < n, with the host libc's
+ * rand() (glibc on the reference's Linux build). */
+void spt_seed_fill(uint32_t *seeds, size_t n, unsigned seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,159 @@
+// rt_api.hip -- runtime part of the C-ABI (include/rt_hip.h): device
+// selection, error reporting, cached device buffers.  The reference's OpenCL
+// hosts print and exit(-1) on any failure (openCLcode.cpp:52-55,
+// smallptGPU.cpp:77-81); this boundary returns status codes instead and the
+// drop-in shims (shim_*.cpp) restore the print-and-exit behaviour.
+#include <mutex>
+#include <stdlib.h>
+#include <stdio.h>
+#include <string.h>
+#include "rt_runtime.h"
+
+namespace rtrt {
+
+namespace {
+thread_local char g_err[512] = "";
+thread_local int g_dev = -1;
+std::mutex g_mu;
+DeviceState *g_states[64] = {};
+
+void release_state(DeviceState *st)
+{
+    if (!st) return;
+    (void)hipSetDevice(st->device);
+    if (st->stream) (void)hipStreamSynchronize(st->stream);
+    for (int i = 0; i < NSCRATCH; i++)
+        if (st->buf[i]) (void)hipFree(st->buf[i]);
+    if (st->stream) (void)hipStreamDestroy(st->stream);
+    delete st;
+}
+}  // namespace
+
+int fail(int code, const char *msg)
+{
+    snprintf(g_err, sizeof(g_err), "%s", msg);
+    return code;
+}
+
+int fail_hip(hipError_t e, const char *what)
+{
+    snprintf(g_err, sizeof(g_err), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+    return RT_ERR_HIP;
+}
+
+int check_launch(const char *what)
+{
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RT_OK : fail_hip(e, what);
+}
+
+int state(DeviceState **out)
+{
+    int dev = g_dev;
+    if (dev < 0) {
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return fail_hip(e, "hipGetDevice");
+    }
+    if (dev < 0 || dev >= 64) return fail(RT_ERR_NODEVICE, "device index out of range");
+    std::lock_guard<std::mutex> lk(g_mu);
+    DeviceState *st = g_states[dev];
+    if (!st) {
+        hipError_t e = hipSetDevice(dev);
+        if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
+        hipDeviceProp_t prop;
+        e = hipGetDeviceProperties(&prop, dev);
+        if (e != hipSuccess) return fail_hip(e, "hipGetDeviceProperties");
+        if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            char m[160];
+            snprintf(m, sizeof(m), "device %d is %s; these kernels are built for gfx950 only", dev,
+                     prop.gcnArchName);
+            return fail(RT_ERR_NODEVICE, m);
+        }
+        st = new DeviceState();
+        st->device = dev;
+        e = hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) { delete st; return fail_hip(e, "hipStreamCreate"); }
+        g_states[dev] = st;
+    } else {
+        hipError_t e = hipSetDevice(dev);
+        if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
+    }
+    *out = st;
+    return RT_OK;
+}
+
+int scratch(DeviceState &st, int slot, size_t bytes, void **out)
+{
+    if (slot < 0 || slot >= NSCRATCH) return fail(RT_ERR_INVALID, "scratch slot");
+    if (bytes == 0) bytes = 16;
+    if (st.cap[slot] < bytes) {
+        if (st.buf[slot]) {
+            hipError_t e = hipStreamSynchronize(st.stream);
+            if (e != hipSuccess) return fail_hip(e, "scratch sync");
+            (void)hipFree(st.buf[slot]);
+            st.cached_bytes -= st.cap[slot];
+            st.buf[slot] = nullptr;
+            st.cap[slot] = 0;
+        }
+        hipError_t e = hipMalloc(&st.buf[slot], bytes);
+        if (e != hipSuccess) { st.buf[slot] = nullptr; return fail_hip(e, "hipMalloc"); }
+        st.cap[slot] = bytes;
+        st.cached_bytes += bytes;
+    }
+    *out = st.buf[slot];
+    return RT_OK;
+}
+
+}  // namespace rtrt
+
+extern "C" const char *rt_last_error(void) { return rtrt::g_err; }
+
+extern "C" int rt_device_count(void)
+{
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "hipGetDeviceCount");
+    return n;
+}
+
+extern "C" int rt_set_device(int device)
+{
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "hipGetDeviceCount");
+    if (device < 0 || device >= n) return rtrt::fail(RT_ERR_NODEVICE, "rt_set_device: no such device");
+    e = hipSetDevice(device);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "hipSetDevice");
+    rtrt::g_dev = device;
+    return RT_OK;
+}
+
+extern "C" int rt_release(void)
+{
+    std::lock_guard<std::mutex> lk(rtrt::g_mu);
+    for (int d = 0; d < 64; d++) {
+        if (rtrt::g_states[d]) {
+            rtrt::release_state(rtrt::g_states[d]);
+            rtrt::g_states[d] = nullptr;
+        }
+    }
+    return RT_OK;
+}
+
+extern "C" size_t rt_cached_bytes(void)
+{
+    std::lock_guard<std::mutex> lk(rtrt::g_mu);
+    size_t s = 0;
+    for (int d = 0; d < 64; d++)
+        if (rtrt::g_states[d]) s += rtrt::g_states[d]->cached_bytes;
+    return s;
+}
+
+extern "C" void spt_seed_fill(uint32_t *seeds, size_t n, unsigned seed)
+{
+    srand(seed);
+    for (size_t i = 0; i < n; i++) {
+        seeds[i] = (uint32_t)rand();
+        if (seeds[i] < 2) seeds[i] = 2;
+    }
+}

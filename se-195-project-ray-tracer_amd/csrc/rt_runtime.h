@@ -1,0 +1,40 @@
+// rt_runtime.h -- host-side runtime of the C-ABI: per-thread error text,
+// per-device state (stream, cached device buffers of the blocking entry
+// points), HIP error mapping.  Defined in rt_api.hip.
+#ifndef RT_RUNTIME_H
+#define RT_RUNTIME_H
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include "../../include/rt_hip.h"
+
+namespace rtrt {
+
+constexpr int NSCRATCH = 8;
+constexpr int SLOT_VIEW = 7;
+
+struct DeviceState {
+    int device = -1;
+    hipStream_t stream = nullptr;      // stream of the blocking entry points
+    void *buf[NSCRATCH] = {};          // grow-only device buffers
+    size_t cap[NSCRATCH] = {};
+    size_t cached_bytes = 0;
+    // Whitted m_SX/m_SY tables for frame size (vt_w, vt_h) in scratch slot
+    // SLOT_VIEW (whitted.hip).
+    int vt_w = 0, vt_h = 0;
+    float vt_DX = 0.f, vt_DY = 0.f;
+};
+
+// Records msg (plus the HIP error string) for rt_last_error(); returns code.
+int fail(int code, const char *msg);
+int fail_hip(hipError_t e, const char *what);
+// hipGetLastError() after a launch, mapped to RT_ERR_HIP.
+int check_launch(const char *what);
+// State of the calling thread's current device (created on first use).
+int state(DeviceState **out);
+// Device buffer slot `slot` of at least `bytes` (grow-only, reused).
+int scratch(DeviceState &st, int slot, size_t bytes, void **out);
+
+}  // namespace rtrt
+
+#endif

@@ -1,0 +1,506 @@
+// smallpt.hip -- gfx950 kernel for the Monte-Carlo hot path of smallptgpu-v1.6.
+//
+// Computes what nsamples successive UpdateRenderingCPU passes
+// (smallptCPU.cpp:77-132) compute: per pixel a camera ray from the pixel's
+// own MWC RNG (simplernd.h:34-48), RadiancePathTracing (geomfunc.h:167-338)
+// or RadianceDirectLighting (:340-483), the running average into the
+// flipped colour slot (smallptCPU.cpp:110-118) and the toInt pack
+// (vec.h:62, smallptCPU.cpp:120-122).  Results match the CPU path bit for bit
+// (the float ops are the reference's, in its order; glibc sinf/cosf/powf are
+// reproduced by rt_glibc_math.h), well inside the 1e-4 HDR tolerance.
+//
+// Mapping (MI355X-first, not a port of rendering_kernel.cl):
+//   * one lane per pixel, a wave per 8x8 tile, 256-thread blocks (16x16);
+//   * ALL samples of a launch run in-lane with path regeneration: the per-
+//     lane loop advances one bounce per iteration and a lane whose path ended
+//     immediately starts its next sample, so a wave's cost is the max over
+//     lanes of the total bounces of nsamples paths (~ the mean for spp >> 1),
+//     not the sum over samples of the per-sample max;
+//   * RNG state, the colour accumulator and the path state stay in VGPRs for
+//     the whole launch: HBM traffic is 32 B per pixel per launch, whatever
+//     nsamples is;
+//   * spheres are staged once per block into LDS as SoA float4 (centre,
+//     rad^2) + material records and read with wave-uniform indices (LDS
+//     broadcast); scenes larger than the LDS budget are read from global
+//     memory through the same wave-uniform loop (L2/scalar-cache resident).
+#include "rt_common.h"
+#include "rt_glibc_math.h"
+
+namespace rt {
+namespace smallpt {
+
+constexpr int MAXS_LDS = 2048;           // LDS copy sized to n: 52 B per sphere, <= 104 KB
+constexpr float EPS = 0.01f;             // geom.h:29
+constexpr float PI_F = 3.14159265358979323846f;
+constexpr int DIFF = 0, SPEC = 1;   // REFR = 2 is the remaining case
+
+struct SphereGeo { float4 g; };          // centre.xyz, rad*rad (same float product as :42)
+
+__device__ __forceinline__ float get_random(uint32_t &s0, uint32_t &s1)   // simplernd.h:34-48
+{
+    s0 = 36969u * (s0 & 65535u) + (s0 >> 16);
+    s1 = 18000u * (s1 & 65535u) + (s1 >> 16);
+    const uint32_t ires = (s0 << 16) + s1;
+    const float f = __uint_as_float((ires & 0x007fffffu) | 0x40000000u);
+    return (f - 2.f) / 2.f;
+}
+
+__device__ __forceinline__ float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ v3 vsmul(float k, v3 b) { return mk(k * b.x, k * b.y, k * b.z); }
+__device__ __forceinline__ v3 vadd(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ v3 vsub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ v3 vmul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ v3 vnorm(v3 v) { const float l = 1.f / sqrtf(vdot(v, v)); return vsmul(l, v); }
+__device__ __forceinline__ v3 vxcross(v3 a, v3 b)
+{
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+
+// SphereIntersect, geomfunc.h:32-59 (g = centre.xyz, rad*rad).
+__device__ __forceinline__ float sphere_hit(float4 g, const ray3 &r)
+{
+    const float opx = g.x - r.o.x, opy = g.y - r.o.y, opz = g.z - r.o.z;
+    const float b = opx * r.d.x + opy * r.d.y + opz * r.d.z;
+    float det = b * b - (opx * opx + opy * opy + opz * opz) + g.w;
+    if (det < 0.f) return 0.f;
+    det = sqrtf(det);
+    float t = b - det;
+    if (t > EPS) return t;
+    t = b + det;
+    return t > EPS ? t : 0.f;
+}
+
+struct Scene {                // per-block LDS copy (or global view for big scenes)
+    const float4 *geo;        // centre, rad^2
+    const float4 *emi;        // emission.xyz, refl (as int bits)
+    const float4 *col;        // colour.xyz, rad
+    const int *lights;        // indices with !viszero(e), ascending
+    int n, nlights;
+};
+
+// Intersect, geomfunc.h:71-92: i descending, update iff d != 0 && d < t.
+__device__ __forceinline__ bool intersect(const Scene &S, const ray3 &r, float &t, int &id)
+{
+    const float inf = 1e20f;
+    t = inf;
+    id = 0;
+    for (int i = S.n - 1; i >= 0; i--) {
+        const float d = sphere_hit(S.geo[i], r);
+        if ((d != 0.f) && (d < t)) { t = d; id = i; }
+    }
+    return t < inf;
+}
+
+// IntersectP, geomfunc.h:94-110 (returns tests performed through ntests).
+__device__ __forceinline__ bool intersect_p(const Scene &S, const ray3 &r, float maxt, unsigned &ntests)
+{
+    for (int i = S.n - 1; i >= 0; i--) {
+        ntests++;
+        const float d = sphere_hit(S.geo[i], r);
+        if ((d != 0.f) && (d < maxt)) return true;
+    }
+    return false;
+}
+
+struct Counts { unsigned long long isect, isectp, tests, samples; };
+
+// SampleLights, geomfunc.h:112-165.  UniformSampleSphere's two GetRandom()
+// arguments are drawn second-first, as the g++-built oracle does (:138).
+__device__ __forceinline__ v3 sample_lights(const Scene &S, uint32_t &s0, uint32_t &s1, v3 hit,
+                                            v3 nl, Counts &cnt)
+{
+    v3 result = mk(0.f, 0.f, 0.f);
+    for (int li = 0; li < S.nlights; li++) {
+        const int i = S.lights[li];
+        const float4 lc = S.col[i];          // colour.xyz, rad
+        const float4 lg = S.geo[i];          // centre
+        const float4 le = S.emi[i];
+        const float rad = lc.w;
+        const float u2 = get_random(s0, s1);
+        const float u1 = get_random(s0, s1);
+        // UniformSampleSphere, geomfunc.h:61-69
+        const float zz = 1.f - 2.f * u1;
+        const float q = 1.f - zz * zz;
+        const float rr = sqrtf((0.f > q) ? 0.f : q);
+        const float phi = 2.f * PI_F * u2;
+        const v3 unit = mk(rr * rtm::cosf(phi), rr * rtm::sinf(phi), zz);
+        v3 sp = vsmul(rad, unit);
+        sp = vadd(sp, mk(lg.x, lg.y, lg.z));
+        ray3 sh;
+        sh.o = hit;
+        sh.d = vsub(sp, hit);
+        const float len = sqrtf(vdot(sh.d, sh.d));
+        sh.d = vsmul(1.f / len, sh.d);
+        float wo = vdot(sh.d, unit);
+        if (wo > 0.f) continue;
+        wo = -wo;
+        const float wi = vdot(sh.d, nl);
+        if (wi > 0.f) {
+            unsigned nt = 0;
+            cnt.isectp++;
+            const bool occluded = intersect_p(S, sh, len - EPS, nt);
+            cnt.tests += nt;
+            if (!occluded) {
+                const float s = (4.f * PI_F * rad * rad) * wi * wo / (len * len);
+                result = vadd(result, vsmul(s, mk(le.x, le.y, le.z)));
+            }
+        }
+    }
+    return result;
+}
+
+// toInt, vec.h:62 (clamp macro keeps -0.0; glibc powf via rt_glibc_math.h).
+__device__ __forceinline__ int to_int(float x)
+{
+    const float c = (x < 0.f) ? 0.f : ((x > 1.f) ? 1.f : x);
+    return (int)(rtm::powf(c, 1.f / 2.2f) * 255.f + .5f);
+}
+
+template <bool DL, bool COUNT, bool LDS>
+__global__ void __launch_bounds__(256)
+render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
+              float *__restrict__ colors, const uint32_t *seeds_in,
+              uint32_t *seeds_out, uint32_t *__restrict__ pixels, int w, int h,
+              int row_begin, int row_end, int first_sample, int nsamples,
+              const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
+              const float4 *__restrict__ g_col, const int *__restrict__ g_lights, int g_nlights,
+              unsigned long long *__restrict__ counters)
+{
+    // Dynamic LDS carve (16-B aligned base, 16-B multiples): geo | emi | col | lights | count
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    Scene S;
+    if (LDS) {
+        float4 *s_geo = (float4 *)smem;
+        float4 *s_emi = s_geo + nspheres;
+        float4 *s_col = s_emi + nspheres;
+        int *s_lights = (int *)(s_col + nspheres);
+        int &s_nl = s_lights[nspheres];
+        for (int i = threadIdx.x; i < nspheres; i += blockDim.x) {
+            const rt_sphere &q = spheres[i];
+            s_geo[i] = make_float4(q.p.x, q.p.y, q.p.z, q.rad * q.rad);
+            s_emi[i] = make_float4(q.e.x, q.e.y, q.e.z, __int_as_float(q.refl));
+            s_col[i] = make_float4(q.c.x, q.c.y, q.c.z, q.rad);
+        }
+        if (threadIdx.x == 0) {
+            int nl = 0;
+            for (int i = 0; i < nspheres; i++) {   // !viszero(e): tests e.x twice (vec.h:44)
+                const rt_sphere &q = spheres[i];
+                if (!((q.e.x == 0.f) && (q.e.x == 0.f) && (q.e.z == 0.f))) s_lights[nl++] = i;
+            }
+            s_nl = nl;
+        }
+        __syncthreads();
+        S.geo = s_geo; S.emi = s_emi; S.col = s_col; S.lights = s_lights; S.nlights = s_nl;
+    } else {
+        S.geo = g_geo; S.emi = g_emi; S.col = g_col; S.lights = g_lights; S.nlights = g_nlights;
+    }
+    S.n = nspheres;
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int y = row_begin + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool active = x < w && y < row_end;
+
+    Counts cnt = {0, 0, 0, 0};
+    if (active) {
+        const int i = (h - y - 1) * w + x;                      // smallptCPU.cpp:86
+        uint32_t s0 = seeds_in[2 * (size_t)i], s1 = seeds_in[2 * (size_t)i + 1];
+        v3 col = mk(0.f, 0.f, 0.f);
+        if (first_sample > 0)
+            col = mk(colors[3 * (size_t)i], colors[3 * (size_t)i + 1], colors[3 * (size_t)i + 2]);
+        const float invW = 1.f / w, invH = 1.f / h;             // :80-81
+
+        int k = 0;
+        bool fresh = true;
+        ray3 ray;
+        v3 rad = mk(0.f, 0.f, 0.f), thr = mk(1.f, 1.f, 1.f);
+        int depth = 0;
+        bool specular = true;
+        while (k < nsamples) {
+            if (fresh) {                                        // :89-105 camera ray
+                const float r1 = get_random(s0, s1) - .5f;
+                const float r2 = get_random(s0, s1) - .5f;
+                const float kcx = (x + r1) * invW - .5f;
+                const float kcy = (y + r2) * invH - .5f;
+                v3 rdir = mk(cam.x.x * kcx + cam.y.x * kcy + cam.dir.x,
+                             cam.x.y * kcx + cam.y.y * kcy + cam.dir.y,
+                             cam.x.z * kcx + cam.y.z * kcy + cam.dir.z);
+                v3 rorig = vsmul(0.1f, rdir);
+                rorig = vadd(rorig, mk(cam.orig.x, cam.orig.y, cam.orig.z));
+                rdir = vnorm(rdir);
+                ray.o = rorig; ray.d = rdir;
+                rad = mk(0.f, 0.f, 0.f);
+                thr = mk(1.f, 1.f, 1.f);
+                depth = 0;
+                specular = true;
+                fresh = false;
+            }
+            // One bounce of geomfunc.h:182-337.
+            bool done = depth > 6;
+            if (!done) {
+                float t;
+                int id;
+                cnt.isect++;
+                cnt.tests += S.n;
+                if (!intersect(S, ray, t, id)) {
+                    done = true;
+                } else {
+                    const float4 og = S.geo[id], oe = S.emi[id], oc = S.col[id];
+                    v3 hit = vsmul(t, ray.d);
+                    hit = vadd(ray.o, hit);
+                    v3 normal = vsub(hit, mk(og.x, og.y, og.z));
+                    normal = vnorm(normal);
+                    const float dp = vdot(normal, ray.d);
+                    const float inv_sign = -1.f * (dp > 0 ? 1.f : -1.f);
+                    const v3 nl = vsmul(inv_sign, normal);
+                    const int refl = __float_as_int(oe.w);
+                    if (!((oe.x == 0.f) && (oe.x == 0.f) && (oe.z == 0.f))) {
+                        if (specular) {
+                            v3 e = vsmul(fabsf(dp), mk(oe.x, oe.y, oe.z));
+                            e = vmul(thr, e);
+                            rad = vadd(rad, e);
+                        }
+                        done = true;
+                    } else if (refl == DIFF) {
+                        specular = false;
+                        thr = vmul(thr, mk(oc.x, oc.y, oc.z));
+                        v3 ld = sample_lights(S, s0, s1, hit, nl, cnt);
+                        ld = vmul(thr, ld);
+                        rad = vadd(rad, ld);
+                        if (DL) {
+                            done = true;
+                        } else {
+                            const float r1 = 2.f * PI_F * get_random(s0, s1);
+                            const float r2 = get_random(s0, s1);
+                            const float r2s = sqrtf(r2);
+                            const v3 wv = nl;
+                            const v3 a = (fabsf(wv.x) > .1f) ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
+                            v3 u = vnorm(vxcross(a, wv));
+                            v3 v = vxcross(wv, u);
+                            u = vsmul(rtm::cosf(r1) * r2s, u);
+                            v = vsmul(rtm::sinf(r1) * r2s, v);
+                            v3 nd = vadd(u, v);
+                            nd = vadd(nd, vsmul(sqrtf(1 - r2), wv));
+                            ray.o = hit;
+                            ray.d = nd;
+                        }
+                    } else if (refl == SPEC) {
+                        specular = true;
+                        v3 nd = vsmul(2.f * vdot(normal, ray.d), normal);
+                        nd = vsub(ray.d, nd);
+                        thr = vmul(thr, mk(oc.x, oc.y, oc.z));
+                        ray.o = hit;
+                        ray.d = nd;
+                    } else {
+                        specular = true;
+                        v3 nd = vsmul(2.f * vdot(normal, ray.d), normal);
+                        nd = vsub(ray.d, nd);
+                        const bool into = vdot(normal, nl) > 0;
+                        const float nc = 1.f, nt = 1.5f;
+                        const float nnt = into ? nc / nt : nt / nc;
+                        const float ddn = vdot(ray.d, nl);
+                        const float cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
+                        if (cos2t < 0.f) {
+                            thr = vmul(thr, mk(oc.x, oc.y, oc.z));
+                            ray.o = hit;
+                            ray.d = nd;
+                        } else {
+                            const float kk = (into ? 1.f : -1.f) * (ddn * nnt + sqrtf(cos2t));
+                            const v3 nkk = vsmul(kk, normal);
+                            v3 td = vsmul(nnt, ray.d);
+                            td = vsub(td, nkk);
+                            td = vnorm(td);
+                            const float a = nt - nc, b = nt + nc;
+                            const float R0 = a * a / (b * b);
+                            const float c = 1 - (into ? -ddn : vdot(td, normal));
+                            const float Re = R0 + (1 - R0) * c * c * c * c * c;
+                            const float Tr = 1.f - Re;
+                            const float P = .25f + .5f * Re;
+                            const float RP = Re / P;
+                            const float TP = Tr / (1.f - P);
+                            if (get_random(s0, s1) < P) {
+                                thr = vsmul(RP, thr);
+                                thr = vmul(thr, mk(oc.x, oc.y, oc.z));
+                                ray.o = hit;
+                                ray.d = nd;
+                            } else {
+                                thr = vsmul(TP, thr);
+                                thr = vmul(thr, mk(oc.x, oc.y, oc.z));
+                                ray.o = hit;
+                                ray.d = td;
+                            }
+                        }
+                    }
+                    depth++;
+                }
+            }
+            if (done) {                                         // :110-118 running average
+                const int current = first_sample + k;
+                if (current == 0) {
+                    col = rad;
+                } else {
+                    const float k1 = (float)current;
+                    const float k2 = 1.f / (k1 + 1.f);
+                    col.x = (col.x * k1 + rad.x) * k2;
+                    col.y = (col.y * k1 + rad.y) * k2;
+                    col.z = (col.z * k1 + rad.z) * k2;
+                }
+                cnt.samples++;
+                k++;
+                fresh = true;
+            }
+        }
+        if (nsamples > 0) {
+            colors[3 * (size_t)i] = col.x;
+            colors[3 * (size_t)i + 1] = col.y;
+            colors[3 * (size_t)i + 2] = col.z;
+            pixels[(size_t)y * w + x] =
+                (uint32_t)(to_int(col.x) | (to_int(col.y) << 8) | (to_int(col.z) << 16));
+        }
+        seeds_out[2 * (size_t)i] = s0;
+        seeds_out[2 * (size_t)i + 1] = s1;
+    }
+    if (COUNT) {
+        const unsigned long long c[4] = {cnt.isect, cnt.isectp, cnt.tests, cnt.samples};
+        flush_counters<4>(counters, c);
+    }
+}
+
+// Global-memory SoA of the scene for scenes above MAXS_LDS.
+__global__ void prepare_kernel(const rt_sphere *__restrict__ spheres, int n, float4 *geo, float4 *emi,
+                               float4 *col, int *lights, int *nlights)
+{
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const rt_sphere &q = spheres[i];
+        geo[i] = make_float4(q.p.x, q.p.y, q.p.z, q.rad * q.rad);
+        emi[i] = make_float4(q.e.x, q.e.y, q.e.z, __int_as_float(q.refl));
+        col[i] = make_float4(q.c.x, q.c.y, q.c.z, q.rad);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int nl = 0;
+        for (int i = 0; i < n; i++) {
+            const rt_sphere &q = spheres[i];
+            if (!((q.e.x == 0.f) && (q.e.x == 0.f) && (q.e.z == 0.f))) lights[nl++] = i;
+        }
+        *nlights = nl;
+    }
+}
+
+}  // namespace smallpt
+}  // namespace rt
+
+// ------------------------------------------------------------------ host side
+#include "rt_runtime.h"
+
+namespace {
+
+template <bool DL, bool COUNT, bool LDS>
+void launch(dim3 grid, hipStream_t s, const rt_sphere *d_spheres, int n, const rt_camera &cam,
+            float *colors, const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h,
+            int r0, int r1, int first, int ns, const float4 *gg, const float4 *ge, const float4 *gc,
+            const int *gl, int gnl, unsigned long long *cnt)
+{
+    const size_t lds = LDS ? (size_t)n * 3 * sizeof(float4) + (size_t)(n + 1) * sizeof(int) : 0;
+    hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, LDS>), grid, dim3(256), lds, s, d_spheres,
+                       n, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, gg, ge, gc, gl, gnl,
+                       cnt);
+}
+
+}  // namespace
+
+extern "C" int spt_render_async(const rt_sphere *d_spheres, unsigned nspheres, const rt_camera *camera,
+                                float *d_colors, const uint32_t *d_seeds_in, uint32_t *d_seeds_out,
+                                uint32_t *d_pixels, int w, int h, int row_begin, int row_end,
+                                int first_sample, int nsamples, int mode, uint64_t *d_counters,
+                                void *stream)
+{
+    if (!d_spheres || !camera || !d_colors || !d_seeds_in || !d_seeds_out || !d_pixels)
+        return rtrt::fail(RT_ERR_INVALID, "spt_render_async: null pointer");
+    if (nspheres < 1 || nspheres > (1u << 24) || w < 1 || h < 1 || first_sample < 0 || nsamples < 0)
+        return rtrt::fail(RT_ERR_INVALID, "spt_render_async: bad sizes");
+    if (row_begin < 0 || row_end > h || row_begin > row_end)
+        return rtrt::fail(RT_ERR_INVALID, "spt_render_async: bad row range");
+    if (mode != SPT_PATH_TRACING && mode != SPT_DIRECT_LIGHTING)
+        return rtrt::fail(RT_ERR_INVALID, "spt_render_async: bad mode");
+    if (row_begin == row_end) return RT_OK;
+    rtrt::DeviceState *st;
+    int rc = rtrt::state(&st);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int n = (int)nspheres;
+    const bool lds = n <= rt::smallpt::MAXS_LDS;
+    const float4 *gg = nullptr, *ge = nullptr, *gc = nullptr;
+    const int *gl = nullptr;
+    int gnl = 0;
+    if (!lds) {
+        // Large scene: SoA copy in global memory (slot 6), light count read back once.
+        void *buf;
+        const size_t bytes = (size_t)n * (3 * sizeof(float4) + sizeof(int)) + 16;
+        if ((rc = rtrt::scratch(*st, 6, bytes, &buf))) return rc;
+        float4 *geo = (float4 *)buf, *emi = geo + n, *col = emi + n;
+        int *lights = (int *)(col + n);
+        int *nl = lights + n;
+        hipLaunchKernelGGL(rt::smallpt::prepare_kernel, dim3(64), dim3(256), 0, s, d_spheres, n, geo, emi,
+                           col, lights, nl);
+        if ((rc = rtrt::check_launch("spt prepare_kernel"))) return rc;
+        hipError_t e = hipMemcpyAsync(&gnl, nl, sizeof(int), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return rtrt::fail_hip(e, "spt light count");
+        gg = geo; ge = emi; gc = col; gl = lights;
+    }
+    dim3 grid((w + 15) / 16, (row_end - row_begin + 15) / 16);
+    unsigned long long *cnt = (unsigned long long *)d_counters;
+    const rt_camera &cam = *camera;
+#define RT_SPT_LAUNCH(DL, C, L)                                                                        \
+    launch<DL, C, L>(grid, s, d_spheres, n, cam, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h,   \
+                     row_begin, row_end, first_sample, nsamples, gg, ge, gc, gl, gnl, cnt)
+    const bool dl = mode == SPT_DIRECT_LIGHTING;
+    if (lds) {
+        if (dl) { if (cnt) RT_SPT_LAUNCH(true, true, true); else RT_SPT_LAUNCH(true, false, true); }
+        else    { if (cnt) RT_SPT_LAUNCH(false, true, true); else RT_SPT_LAUNCH(false, false, true); }
+    } else {
+        if (dl) { if (cnt) RT_SPT_LAUNCH(true, true, false); else RT_SPT_LAUNCH(true, false, false); }
+        else    { if (cnt) RT_SPT_LAUNCH(false, true, false); else RT_SPT_LAUNCH(false, false, false); }
+    }
+#undef RT_SPT_LAUNCH
+    return rtrt::check_launch("spt render_kernel");
+}
+
+extern "C" int spt_render(const rt_sphere *spheres, unsigned nspheres, const rt_camera *camera,
+                          float *colors, uint32_t *seeds, uint32_t *pixels, int w, int h,
+                          int first_sample, int nsamples, int mode, uint64_t *counters)
+{
+    if (!spheres || !camera || !colors || !seeds || !pixels || w < 1 || h < 1 || nspheres < 1)
+        return rtrt::fail(RT_ERR_INVALID, "spt_render: bad arguments");
+    rtrt::DeviceState *st;
+    int rc = rtrt::state(&st);
+    if (rc) return rc;
+    const size_t npx = (size_t)w * h;
+    void *d_s, *d_col, *d_seed, *d_px, *d_cnt;
+    if ((rc = rtrt::scratch(*st, 0, sizeof(rt_sphere) * nspheres, &d_s))) return rc;
+    if ((rc = rtrt::scratch(*st, 1, 3 * sizeof(float) * npx, &d_col))) return rc;
+    if ((rc = rtrt::scratch(*st, 2, 2 * sizeof(uint32_t) * npx, &d_seed))) return rc;
+    if ((rc = rtrt::scratch(*st, 3, sizeof(uint32_t) * npx, &d_px))) return rc;
+    if ((rc = rtrt::scratch(*st, 4, 4 * sizeof(uint64_t), &d_cnt))) return rc;
+    hipStream_t s = st->stream;
+    hipError_t e = hipMemcpyAsync(d_s, spheres, sizeof(rt_sphere) * nspheres, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_seed, seeds, 2 * sizeof(uint32_t) * npx, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && first_sample > 0)
+        e = hipMemcpyAsync(d_col, colors, 3 * sizeof(float) * npx, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && counters) e = hipMemsetAsync(d_cnt, 0, 4 * sizeof(uint64_t), s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "spt_render H2D");
+    rc = spt_render_async((const rt_sphere *)d_s, nspheres, camera, (float *)d_col, (uint32_t *)d_seed,
+                          (uint32_t *)d_seed, (uint32_t *)d_px, w, h, 0, h, first_sample, nsamples, mode,
+                          counters ? (uint64_t *)d_cnt : nullptr, s);
+    if (rc) return rc;
+    e = hipMemcpyAsync(seeds, d_seed, 2 * sizeof(uint32_t) * npx, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && nsamples > 0) {
+        e = hipMemcpyAsync(colors, d_col, 3 * sizeof(float) * npx, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(pixels, d_px, sizeof(uint32_t) * npx, hipMemcpyDeviceToHost, s);
+    }
+    if (e == hipSuccess && counters)
+        e = hipMemcpyAsync(counters, d_cnt, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "spt_render D2H");
+    return RT_OK;
+}

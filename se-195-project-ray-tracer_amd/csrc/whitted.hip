@@ -1,0 +1,483 @@
+// whitted.hip -- gfx950 kernel for the Whitted hot path of raytracer3.0.06.no_rec.samp.
+//
+// Computes, bit for bit, what the CPU path Engine_Render (raytracer.cpp:301-530)
+// writes into the Surface framebuffer: per pixel 3x3 primary sub-samples, each
+// expanded into the reference's 63-node breadth-first ray tree
+// (raytracer.cpp:398-472), back-accumulated (:476-511), summed (:513-515) and
+// packed to 0x00RRGGBB with the x28 scale and 255 clamp (:517-523).
+//
+// Mapping (MI355X-first, not a port of openCLcode.cl):
+//   * one lane per pixel; a wave owns an 8x8 pixel tile (coherent trees),
+//     a 256-thread block a 16x16 tile;
+//   * the <= 64 primitives are staged once per block from the reference's
+//     96-byte AoS into LDS as SoA (geometry float4, materials, light list);
+//     the nearest-hit and occluder loops read them with wave-uniform indices
+//     (LDS broadcast, no bank conflicts);
+//   * the ray tree runs in the reference's breadth-first order from a 64-bit
+//     "to do" mask (ctz = next node), so the stale-refraction-ray quirk after
+//     total internal reflection (raytracer.cpp:231-233) is reproduced
+//     exactly; the nine sub-samples and their trees form ONE per-lane work
+//     loop (a lane that finishes a small tree starts its next sub-sample
+//     while others still trace), so a wave's cost is the max over lanes of
+//     the whole pixel's traced rays, not of each sub-sample's;
+//   * per-node tree records live in per-lane private memory (touched only for
+//     traced nodes); the running ray, its shading and the occluder loops stay
+//     in VGPRs;
+//   * m_SX / m_SY are sequential float sums in the reference (:309,:524,:526):
+//     the host tabulates them once per frame size (exact same float adds);
+//   * glibc powf/expf are reproduced by rt_glibc_math.h (double-precision,
+//     op-for-op restatement of glibc 2.35's FMA build).
+#include "rt_common.h"
+#include "rt_glibc_math.h"
+
+namespace rt {
+namespace whitted {
+
+constexpr int MAXP = 64;        // reference allocates 50 (scene.cpp:225)
+constexpr int NODES = 63;       // raytracer.cpp:336
+constexpr float EPS = 0.001f;   // common.h:24
+constexpr int SPHERE = 1, PLANE = 2;
+
+struct Scene {
+    float4 geo[MAXP];   // sphere: centre.xyz, SqRadius   plane: N.xyz, D
+    float4 mat0[MAXP];  // colour.xyz, refl
+    float4 mat1[MAXP];  // refr, diff, spec, rindex
+    float4 cen[MAXP];   // m_Centre (light position, raytracer.cpp:80,115)
+    float rrad[MAXP];   // RRadius (sphere normal scale)
+    int type[MAXP];
+    int light[MAXP];
+    int nonlight[MAXP]; // indices of m_Light == 0 primitives, in index order
+    int lights[MAXP];   // indices of m_Light > 0 primitives, in index order
+    int n, nnonlight, nlights;
+};
+
+// Primitive_Intersect, scene.cpp:125-190.  Returns HIT 1 / INPRIM -1 / MISS 0.
+__device__ __forceinline__ int intersect(int type, float4 g, const ray3 &r, float &dist)
+{
+    if (type == SPHERE) {
+        float vx = r.o.x - g.x, vy = r.o.y - g.y, vz = r.o.z - g.z;
+        float b = vx * r.d.x + vy * r.d.y + vz * r.d.z;
+        b = -b;
+        float det = (b * b) - (vx * vx + vy * vy + vz * vz) + g.w;
+        int ret = 0;
+        if (det > 0) {
+            det = sqrtf(det);
+            float i1 = b - det, i2 = b + det;
+            if (i2 > 0) {
+                if (i1 < 0) {
+                    if (i2 < dist) { dist = i2; ret = -1; }
+                } else if (i1 < dist) {
+                    dist = i1; ret = 1;
+                }
+            }
+        }
+        return ret;
+    }
+    if (type == PLANE) {
+        float d = g.x * r.d.x + g.y * r.d.y + g.z * r.d.z;
+        if (d != 0) {
+            float t = -((g.x * r.o.x + g.y * r.o.y + g.z * r.o.z) + g.w) / d;
+            if (t > 0 && t < dist) { dist = t; return 1; }
+        }
+    }
+    return 0;
+}
+
+// Primitive_GetNormal, scene.cpp:34-53.
+__device__ __forceinline__ v3 normal_at(const Scene &S, int p, v3 pos)
+{
+    int t = S.type[p];
+    float4 g = S.geo[p];
+    if (t == SPHERE) {
+        float rr = S.rrad[p];
+        v3 n = mk(pos.x - g.x, pos.y - g.y, pos.z - g.z);
+        n.x *= rr; n.y *= rr; n.z *= rr;
+        return n;
+    }
+    if (t == PLANE) return mk(g.x, g.y, g.z);
+    return mk(0.f, 0.f, 0.f);
+}
+
+struct Hit {
+    v3 acc;           // node colour (starts at 0, raytracer.cpp:403-405)
+    int prim;         // nearest primitive, -1 on miss
+    float dist;       // *a_Dist
+    float refl, refr; // *a_refl / *a_refr as the caller sees them
+    bool refr_ray_ok; // refraction ray written (false on TIR)
+    float rindex_out; // *a_RIndex after the call
+    ray3 refl_ray, refr_ray;
+};
+
+struct Counts { unsigned long long traced, shadow, tests, tir; };
+
+// Engine_Raytrace, raytracer.cpp:30-271 (a_Depth is always 1 at every call
+// site, so the TRACEDEPTH guards are constant-true).
+__device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &cnt)
+{
+    Hit h;
+    h.acc = mk(0.f, 0.f, 0.f);
+    h.prim = -1;
+    h.refl = 0.f; h.refr = 0.f;
+    h.refr_ray_ok = false;
+    h.rindex_out = rindex_in;
+    cnt.traced++;
+    float dist = 1000000.0f;
+    int prim = 0, result = 0, hit_once = 0;
+    const int n = S.n;
+    for (int s = 0; s < n; s++) {                       // :39-49 nearest, lowest index on ties
+        int res = intersect(S.type[s], S.geo[s], ray, dist);
+        if (res) { hit_once = 1; prim = s; result = res; }
+    }
+    cnt.tests += (unsigned long long)n;
+    h.dist = dist;
+    if (!hit_once) return h;                            // :51
+    h.prim = prim;
+    if (S.light[prim] > 0) {                            // :53-57
+        h.acc = mk(1.f, 1.f, 1.f);
+        return h;
+    }
+    v3 pi;                                              // :61-65
+    pi.x = ray.d.x * dist; pi.y = ray.d.y * dist; pi.z = ray.d.z * dist;
+    pi.x += ray.o.x; pi.y += ray.o.y; pi.z += ray.o.z;
+
+    const float4 m0 = S.mat0[prim];
+    const float4 m1 = S.mat1[prim];
+    const float pdiff = m1.y, pspec = m1.z;
+    const v3 N = normal_at(S, prim, pi);
+
+    for (int li = 0; li < S.nlights; li++) {            // :68-176 lights in index order
+        const int l = S.lights[li];
+        const float4 lg = S.cen[l];
+        const float4 lm = S.mat0[l];
+        float shade = 1.0f;
+        if (S.type[l] == SPHERE) {                      // :76-110
+            v3 L = mk(lg.x - pi.x, lg.y - pi.y, lg.z - pi.z);
+            float tdist = sqrtf(L.x * L.x + L.y * L.y + L.z * L.z);
+            float inv = 1.0f / tdist;
+            L.x *= inv; L.y *= inv; L.z *= inv;
+            ray3 r;
+            r.o = mk(pi.x + L.x * EPS, pi.y + L.y * EPS, pi.z + L.z * EPS);
+            r.d = L;
+            cnt.shadow++;
+            int k = 0;
+            const int nn = S.nnonlight;
+            for (; k < nn; k++) {                       // first occluder ends the loop
+                const int s = S.nonlight[k];
+                if (intersect(S.type[s], S.geo[s], r, tdist)) { shade = 0; break; }
+            }
+            cnt.tests += (unsigned long long)(k < nn ? k + 1 : nn);
+        }
+        if (shade > 0) {                                // :112-174
+            v3 L = mk(lg.x, lg.y, lg.z);
+            L.x -= pi.x; L.y -= pi.y; L.z -= pi.z;
+            float len = sqrtf(L.x * L.x + L.y * L.y + L.z * L.z);
+            if (len > 0.0f) {
+                float inv = 1.0f / len;
+                L.x *= inv; L.y *= inv; L.z *= inv;
+            } else {
+                L = mk(0.f, 0.f, 0.f);
+            }
+            if (pdiff > 0) {
+                float dot = L.x * N.x + L.y * N.y + L.z * N.z;
+                if (dot > 0) {
+                    float diff = dot * pdiff * shade;
+                    v3 dv = mk(m0.x, m0.y, m0.z);
+                    dv.x *= lm.x; dv.y *= lm.y; dv.z *= lm.z;
+                    dv.x *= diff; dv.y *= diff; dv.z *= diff;
+                    h.acc.x += dv.x; h.acc.y += dv.y; h.acc.z += dv.z;
+                }
+            }
+            if (pspec > 0) {
+                float td = (L.x * N.x + L.y * N.y + L.z * N.z);
+                v3 R = mk(L.x - 2.0f * td * N.x, L.y - 2.0f * td * N.y, L.z - 2.0f * td * N.z);
+                float dot = (ray.d.x * R.x + ray.d.y * R.y + ray.d.z * R.z);
+                if (dot > 0) {
+                    float spec = rtm::powf(dot, 20.0f) * pspec * shade;
+                    h.acc.x += spec * lm.x; h.acc.y += spec * lm.y; h.acc.z += spec * lm.z;
+                }
+            }
+        }
+    }
+
+    h.refr = m1.x;                                      // :181-236
+    if (h.refr > 0) {
+        const float rindex = m1.w;
+        const float nr = rindex_in / rindex;
+        h.rindex_out = rindex;
+        const float fres = (float)result;
+        v3 Nr = mk(N.x * fres, N.y * fres, N.z * fres);
+        float cosI = Nr.x * ray.d.x + Nr.y * ray.d.y + Nr.z * ray.d.z;
+        cosI = -cosI;
+        float cosT2 = 1.0f - nr * nr * (1.0f - cosI * cosI);
+        if (cosT2 > 0.0f) {
+            float k = nr * cosI - sqrtf(cosT2);
+            v3 T = mk((nr * ray.d.x) + k * Nr.x, (nr * ray.d.y) + k * Nr.y, (nr * ray.d.z) + k * Nr.z);
+            h.refr_ray.o = mk(pi.x + T.x * EPS, pi.y + T.y * EPS, pi.z + T.z * EPS);
+            h.refr_ray.d = T;
+            h.refr_ray_ok = true;
+        }
+    }
+
+    h.refl = m0.w;                                      // :241-267
+    if (h.refl > 0.0f) {
+        float dR = (ray.d.x * N.x + ray.d.y * N.y + ray.d.z * N.z);
+        v3 R = mk(ray.d.x - 2.0f * dR * N.x, ray.d.y - 2.0f * dR * N.y, ray.d.z - 2.0f * dR * N.z);
+        h.refl_ray.o = mk(pi.x + R.x * EPS, pi.y + R.y * EPS, pi.z + R.z * EPS);
+        h.refl_ray.d = R;
+    }
+    return h;
+}
+
+// Primary ray of sub-sample `sub` (tx outer, ty inner: raytracer.cpp:351,364-367).
+__device__ __forceinline__ ray3 primary(int sub, float SX, float SY, float DX, float DY)
+{
+    const float tx = (float)(sub / 3 - 1), ty = (float)(sub % 3 - 1);
+    v3 d;
+    d.x = (SX + DX * tx / 2.0f) - 0.0f;
+    d.y = (SY + DY * ty / 2.0f) - 0.25f;
+    d.z = 0.0f - (-7.0f);
+    float l = 1.0f / sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+    d.x *= l; d.y *= l; d.z *= l;
+    ray3 r;
+    r.o = mk(0.0f, 0.25f, -7.0f);
+    r.d = d;
+    return r;
+}
+
+struct NodeStore {       // per-lane private tree records (only traced nodes touched)
+    float4 col[NODES];   // colour.xyz, dist
+    int info[NODES];     // hit primitive | (TIR << 8)
+    float4 ra[NODES];    // refl ray o.xyz, d.x
+    float4 rb[NODES];    // refl ray d.yz, refr ray o.xy
+    float4 rc[NODES];    // refr ray o.z, d.xyz
+    float rin[NODES];    // *a_RIndex after the node's call
+};
+
+template <bool COUNT>
+__global__ void __launch_bounds__(256)
+render_kernel(const rt_primitive *__restrict__ prims, int nprims, uint32_t *__restrict__ out,
+              int w, int row_begin, int row_end, const float *__restrict__ sx_tab,
+              const float *__restrict__ sy_tab, float DX, float DY,
+              unsigned long long *__restrict__ counters)
+{
+    __shared__ Scene S;
+    // Stage the reference's 96-byte AoS primitives into LDS SoA.
+    for (int p = threadIdx.x; p < nprims; p += blockDim.x) {
+        const rt_primitive &q = prims[p];
+        const bool sph = q.type == SPHERE;
+        S.geo[p] = sph ? make_float4(q.m_Centre.x, q.m_Centre.y, q.m_Centre.z, q.m_SqRadius)
+                       : make_float4(q.plane_N.x, q.plane_N.y, q.plane_N.z, q.plane_D);
+        S.mat0[p] = make_float4(q.m_Color.x, q.m_Color.y, q.m_Color.z, q.m_Refl);
+        S.mat1[p] = make_float4(q.m_Refr, q.m_Diff, q.m_Spec, q.m_RIndex);
+        S.cen[p] = make_float4(q.m_Centre.x, q.m_Centre.y, q.m_Centre.z, 0.f);
+        S.rrad[p] = q.m_RRadius;
+        S.type[p] = q.type;
+        S.light[p] = q.m_Light;
+    }
+    if (threadIdx.x == 0) {
+        int nl = 0, nn = 0;
+        for (int p = 0; p < nprims; p++) {
+            if (prims[p].m_Light > 0) S.lights[nl++] = p;
+            if (prims[p].m_Light == 0) S.nonlight[nn++] = p;
+        }
+        S.n = nprims; S.nlights = nl; S.nnonlight = nn;
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int y = row_begin + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool active = x < w && y < row_end;
+
+    Counts cnt = {0, 0, 0, 0};
+    if (active) {
+        const float SX = sx_tab[x], SY = sy_tab[y];
+        NodeStore ns;
+        float tr = 0.f, tg = 0.f, tb = 0.f;
+        int sub = 0;
+        unsigned long long todo = 1, traced = 0;
+        ray3 root = primary(0, SX, SY, DX, DY);
+        ray3 cur_refr = root;              // the caller's refr_Ray variable (:373-374)
+        for (;;) {
+            const int i = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            traced |= 1ull << i;
+            ray3 r;
+            float rin;
+            if (i == 0) {
+                r = root; rin = 1.0f;
+            } else {
+                const int p = (i - 1) >> 1;
+                const float4 a = ns.ra[p], b = ns.rb[p], c = ns.rc[p];
+                if (i & 1) { r.o = mk(a.x, a.y, a.z); r.d = mk(a.w, b.x, b.y); }
+                else       { r.o = mk(b.z, b.w, c.x); r.d = mk(c.y, c.z, c.w); }
+                rin = ns.rin[p];
+            }
+            Hit hh = trace(S, r, rin, cnt);
+            const bool tir = hh.refr > 0 && !hh.refr_ray_ok;
+            ns.col[i] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
+            ns.info[i] = (hh.prim & 0xff) | (tir ? 0x100 : 0);
+            if (hh.refr_ray_ok) cur_refr = hh.refr_ray;
+            if (i < NODES / 2) {
+                if (tir) cnt.tir++;
+                const bool cl = hh.refl > 0, cr = hh.refr > 0;
+                if (cl || cr) {
+                    const ray3 fl = hh.refl_ray, fr = cur_refr;
+                    ns.ra[i] = make_float4(fl.o.x, fl.o.y, fl.o.z, fl.d.x);
+                    ns.rb[i] = make_float4(fl.d.y, fl.d.z, fr.o.x, fr.o.y);
+                    ns.rc[i] = make_float4(fr.o.z, fr.d.x, fr.d.y, fr.d.z);
+                    ns.rin[i] = hh.rindex_out;
+                    if (cl) todo |= 1ull << (2 * i + 1);
+                    if (cr) todo |= 1ull << (2 * i + 2);
+                }
+            }
+            if (todo) continue;
+            // Back-accumulation (:476-511): children in decreasing index order,
+            // refraction child (even) before reflection child (odd).
+            unsigned long long m = traced & ~1ull;
+            while (m) {
+                const int c = 63 - __builtin_clzll(m);
+                m &= ~(1ull << c);
+                const int p = (c - 1) >> 1;
+                const float4 cc = ns.col[c];
+                float4 pc = ns.col[p];
+                const int pinfo = ns.info[p];
+                const int pp = pinfo & 0xff;
+                const float4 pm = S.mat0[pp];
+                float ax = cc.x, ay = cc.y, az = cc.z;
+                if (!(c & 1)) {
+                    if (!(pinfo & 0x100)) {
+                        const float nd = -pc.w;
+                        ax = cc.x * rtm::expf(pm.x * 0.15f * nd);
+                        ay = cc.y * rtm::expf(pm.y * 0.15f * nd);
+                        az = cc.z * rtm::expf(pm.z * 0.15f * nd);
+                    }
+                } else {
+                    ax = cc.x * pm.x * pm.w;
+                    ay = cc.y * pm.y * pm.w;
+                    az = cc.z * pm.z * pm.w;
+                }
+                pc.x += ax; pc.y += ay; pc.z += az;
+                ns.col[p] = pc;
+            }
+            const float4 c0 = ns.col[0];
+            tr += c0.x; tg += c0.y; tb += c0.z;
+            if (++sub == 9) break;
+            root = primary(sub, SX, SY, DX, DY);
+            cur_refr = root;
+            todo = 1;
+            traced = 0;
+        }
+        int red = (int)(tr * 28.0f), green = (int)(tg * 28.0f), blue = (int)(tb * 28.0f);
+        if (red > 255) red = 255;
+        if (green > 255) green = 255;
+        if (blue > 255) blue = 255;
+        out[(size_t)y * w + x] = (uint32_t)((red << 16) + (green << 8) + blue);
+    }
+    if (COUNT) {
+        const unsigned long long c[4] = {cnt.traced, cnt.shadow, cnt.tests, cnt.tir};
+        flush_counters<4>(counters, c);
+    }
+}
+
+}  // namespace whitted
+}  // namespace rt
+
+// ------------------------------------------------------------------ host side
+#include "rt_runtime.h"
+
+namespace {
+
+// m_SX / m_SY tables (Engine_InitRender raytracer.cpp:278-294, then the
+// sequential m_SX += m_DX (:524) and m_SY += m_DY (:526)) -- host float adds,
+// uploaded once per frame size into the device state's SLOT_VIEW buffer.
+int view_tables(rtrt::DeviceState &st, int w, int h, const float **d_sx, const float **d_sy)
+{
+    void *d = nullptr;
+    int rc = rtrt::scratch(st, rtrt::SLOT_VIEW, sizeof(float) * ((size_t)w + h), &d);
+    if (rc) return rc;
+    if (st.vt_w != w || st.vt_h != h) {
+        const float WX1 = -3, WX2 = 3, WY1 = 2.25f, WY2 = -2.25f;
+        const float DX = (WX2 - WX1) / w;
+        const float DY = (WY2 - WY1) / h;
+        float *tab = new float[(size_t)w + h];
+        float sx = WX1;
+        for (int x = 0; x < w; x++) { tab[x] = sx; sx += DX; }
+        float sy = WY1;
+        sy += 20 * DY;
+        for (int y = 0; y < h; y++) tab[w + y] = 0.f;
+        for (int y = 20; y < h; y++) { tab[w + y] = sy; sy += DY; }
+        hipError_t e = hipMemcpy(d, tab, sizeof(float) * ((size_t)w + h), hipMemcpyHostToDevice);
+        delete[] tab;
+        if (e != hipSuccess) return rtrt::fail_hip(e, "whitted view tables");
+        st.vt_w = w; st.vt_h = h; st.vt_DX = DX; st.vt_DY = DY;
+    }
+    *d_sx = (const float *)d;
+    *d_sy = (const float *)d + w;
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" int rtw_render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int w,
+                                int h, int row_begin, int row_end, uint64_t *d_counters,
+                                void *stream)
+{
+    if (!d_prims || !d_xrgb || nprims < 1 || nprims > rt::whitted::MAXP || w < 1 || h < 1)
+        return rtrt::fail(RT_ERR_INVALID, "rtw_render_async: bad arguments");
+    if (row_begin < 20 || row_end > h || row_begin >= row_end)
+        return rtrt::fail(RT_ERR_INVALID, "rtw_render_async: rows must satisfy 20 <= row_begin < row_end <= h");
+    rtrt::DeviceState *st;
+    int rc = rtrt::state(&st);
+    if (rc) return rc;
+    const float *d_sx, *d_sy;
+    rc = view_tables(*st, w, h, &d_sx, &d_sy);
+    if (rc) return rc;
+    const int rows = row_end - row_begin;
+    dim3 grid((w + 15) / 16, (rows + 15) / 16), block(256);
+    hipStream_t s = (hipStream_t)stream;
+    if (d_counters)
+        hipLaunchKernelGGL(rt::whitted::render_kernel<true>, grid, block, 0, s, d_prims, nprims,
+                           d_xrgb, w, row_begin, row_end, d_sx, d_sy, st->vt_DX, st->vt_DY,
+                           (unsigned long long *)d_counters);
+    else
+        hipLaunchKernelGGL(rt::whitted::render_kernel<false>, grid, block, 0, s, d_prims, nprims,
+                           d_xrgb, w, row_begin, row_end, d_sx, d_sy, st->vt_DX, st->vt_DY,
+                           (unsigned long long *)nullptr);
+    return rtrt::check_launch("rtw render_kernel");
+}
+
+extern "C" int rtw_render(const rt_primitive *prims, int nprims, uint32_t *xrgb, int w, int h,
+                          int row_begin, int row_end, uint64_t *counters)
+{
+    if (!prims || !xrgb || nprims < 1 || nprims > rt::whitted::MAXP || w < 1 || h < 1)
+        return rtrt::fail(RT_ERR_INVALID, "rtw_render: bad arguments");
+    if (row_begin < 20 || row_end > h || row_begin >= row_end)
+        return rtrt::fail(RT_ERR_INVALID, "rtw_render: rows must satisfy 20 <= row_begin < row_end <= h");
+    rtrt::DeviceState *st;
+    int rc = rtrt::state(&st);
+    if (rc) return rc;
+    const size_t frame_bytes = sizeof(uint32_t) * (size_t)w * h;
+    void *d_prims, *d_frame, *d_cnt;
+    if ((rc = rtrt::scratch(*st, 0, sizeof(rt_primitive) * nprims, &d_prims))) return rc;
+    if ((rc = rtrt::scratch(*st, 1, frame_bytes, &d_frame))) return rc;
+    if ((rc = rtrt::scratch(*st, 2, 4 * sizeof(uint64_t), &d_cnt))) return rc;
+    hipStream_t s = st->stream;
+    hipError_t e = hipMemcpyAsync(d_prims, prims, sizeof(rt_primitive) * nprims, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render H2D prims");
+    // Rows outside [row_begin,row_end) are left untouched: copy only the window back.
+    if (counters && (e = hipMemsetAsync(d_cnt, 0, 4 * sizeof(uint64_t), s)) != hipSuccess)
+        return rtrt::fail_hip(e, "rtw_render memset");
+    rc = rtw_render_async((const rt_primitive *)d_prims, nprims, (uint32_t *)d_frame, w, h, row_begin,
+                          row_end, counters ? (uint64_t *)d_cnt : nullptr, s);
+    if (rc) return rc;
+    const size_t off = sizeof(uint32_t) * (size_t)row_begin * w;
+    const size_t len = sizeof(uint32_t) * (size_t)(row_end - row_begin) * w;
+    e = hipMemcpyAsync((char *)xrgb + off, (char *)d_frame + off, len, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render D2H frame");
+    if (counters && (e = hipMemcpyAsync(counters, d_cnt, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return rtrt::fail_hip(e, "rtw_render D2H counters");
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render sync");
+    return RT_OK;
+}

@@ -1,0 +1,70 @@
+"""rtamd -- host-side Python binding of the MI355X ray-trace hot path.
+
+Thin ctypes layer over librt_hip.so (include/rt_hip.h).  The C++ drop-in
+shims (csrc/shim_*.cpp) are the reference-facing host API; this module is
+what the tests, bench.py and __graft_entry__ drive.
+
+    Whitted  : whitted_render()  ~ Engine_InitRender + Engine_Render
+               (raytracer3.0.06.no_rec.samp/raytracer.cpp:278-530) on the GPU
+    smallpt  : SmallptFrame.render(k)  ~ k x UpdateRenderingCPU
+               (smallptgpu-v1.6/smallptCPU.cpp:77-132) on the GPU
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import scenes
+from ._lib import (Camera, Primitive, RTError, Sphere, Vec3, check, device_count, lib,
+                   set_device, SPT_DIRECT_LIGHTING, SPT_PATH_TRACING)
+
+__all__ = ["Camera", "Primitive", "Sphere", "Vec3", "RTError", "scenes", "lib", "check",
+           "device_count", "set_device", "whitted_render", "SmallptFrame",
+           "SPT_PATH_TRACING", "SPT_DIRECT_LIGHTING"]
+
+
+def whitted_render(w, h, row_begin=20, row_end=None, prims=None, nprims=None, frame=None,
+                   counters=False):
+    """Render rows [row_begin,row_end) (default the reference window
+    [20, h-70)) into a uint32 [h, w] frame (zero-cleared unless given).
+    Returns frame, or (frame, [traced, shadow, tests, tir]) if counters."""
+    if prims is None:
+        prims, nprims = scenes.whitted_scene()
+    if row_end is None:
+        row_end = h - 70
+    if frame is None:
+        frame = np.zeros((h, w), dtype=np.uint32)
+    assert frame.dtype == np.uint32 and frame.shape == (h, w) and frame.flags.c_contiguous
+    cnt = (C.c_uint64 * 4)()
+    check(lib().rtw_render(C.addressof(prims), nprims, frame.ctypes.data, w, h, row_begin,
+                           row_end, C.addressof(cnt) if counters else None))
+    return (frame, list(cnt)) if counters else frame
+
+
+class SmallptFrame:
+    """Progressive smallpt frame state: colors / seeds / pixels exactly as
+    smallptGPU.cpp's AllocateBuffers lays them out, and currentSample."""
+
+    def __init__(self, w, h, spheres=None, nspheres=None, camera=None, seed=1,
+                 mode=SPT_PATH_TRACING):
+        if spheres is None:
+            spheres, nspheres = scenes.cornell()
+        if camera is None:
+            camera = scenes.cornell_camera(w, h)
+        self.w, self.h = w, h
+        self.spheres, self.nspheres, self.camera, self.mode = spheres, nspheres, camera, mode
+        self.colors = np.zeros(3 * w * h, dtype=np.float32)
+        self.seeds = scenes.seeds(w, h, seed)
+        self.pixels = np.zeros(w * h, dtype=np.uint32)
+        self.current_sample = 0
+        self.counters = [0, 0, 0, 0]
+
+    def render(self, nsamples=1):
+        """nsamples successive UpdateRenderingCPU passes on the GPU."""
+        cnt = (C.c_uint64 * 4)()
+        check(lib().spt_render(C.addressof(self.spheres), self.nspheres, C.byref(self.camera),
+                               self.colors.ctypes.data, self.seeds.ctypes.data,
+                               self.pixels.ctypes.data, self.w, self.h, self.current_sample,
+                               nsamples, self.mode, C.addressof(cnt)))
+        self.current_sample += nsamples
+        self.counters = [a + b for a, b in zip(self.counters, cnt)]
+        return self

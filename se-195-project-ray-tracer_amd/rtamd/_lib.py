@@ -1,0 +1,92 @@
+"""Loader for librt_hip.so (include/rt_hip.h) and the reference struct layouts.
+
+The shared library is built in-tree by ``make -C se-195-project-ray-tracer_amd``
+(``__graft_entry__.build()``).  There is no CPU fallback: if the library or a
+gfx950 device is missing, calls raise :class:`RTError`.
+"""
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
+
+RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NODEVICE = 0, -1, -2, -3
+SPT_PATH_TRACING, SPT_DIRECT_LIGHTING = 0, 1
+
+# Every symbol include/rt_hip.h declares (checked by tests/test_abi.py).
+EXPORTS = ("rt_last_error", "rt_device_count", "rt_set_device", "rt_release", "rt_cached_bytes",
+           "rtw_render", "rtw_render_async", "spt_render", "spt_render_async", "spt_seed_fill")
+
+
+class RTError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (rt code %d)" % (msg, code))
+        self.code = code
+
+
+class Vec3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class Primitive(C.Structure):
+    """raytracer3.0.06.no_rec.samp/raytracer.h:23-32 (96 bytes)."""
+    _fields_ = [("type", C.c_int32), ("m_Light", C.c_int32), ("m_Centre", Vec3),
+                ("m_SqRadius", C.c_float), ("m_Radius", C.c_float), ("m_RRadius", C.c_float),
+                ("plane_N", Vec3), ("plane_D", C.c_float), ("plane_cell", C.c_float * 4),
+                ("m_Color", Vec3), ("m_Refl", C.c_float), ("m_Refr", C.c_float),
+                ("m_Diff", C.c_float), ("m_Spec", C.c_float), ("m_RIndex", C.c_float)]
+
+
+class Sphere(C.Structure):
+    """smallptgpu-v1.6/geom.h:43-47 (44 bytes)."""
+    _fields_ = [("rad", C.c_float), ("p", Vec3), ("e", Vec3), ("c", Vec3), ("refl", C.c_int32)]
+
+
+class Camera(C.Structure):
+    """smallptgpu-v1.6/camera.h:29-34 (60 bytes)."""
+    _fields_ = [("orig", Vec3), ("target", Vec3), ("dir", Vec3), ("x", Vec3), ("y", Vec3)]
+
+
+assert C.sizeof(Primitive) == 96 and C.sizeof(Sphere) == 44 and C.sizeof(Camera) == 60
+
+_lib = None
+
+
+def lib():
+    """The loaded librt_hip.so (raises RTError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RTError(RT_ERR_NODEVICE, "librt_hip.so not built (%s); run "
+                      "`make -C se-195-project-ray-tracer_amd` or __graft_entry__.build()" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    vp, i, u, u64p = C.c_void_p, C.c_int, C.c_uint, C.c_void_p
+    L.rt_last_error.restype = C.c_char_p
+    L.rt_device_count.restype = i
+    L.rt_set_device.argtypes = [i]
+    L.rt_cached_bytes.restype = C.c_size_t
+    L.rtw_render.argtypes = [vp, i, vp, i, i, i, i, u64p]
+    L.rtw_render_async.argtypes = [vp, i, vp, i, i, i, i, u64p, vp]
+    L.spt_render.argtypes = [vp, u, vp, vp, vp, vp, i, i, i, i, i, u64p]
+    L.spt_render_async.argtypes = [vp, u, vp, vp, vp, vp, vp, i, i, i, i, i, i, i, u64p, vp]
+    L.spt_seed_fill.argtypes = [vp, C.c_size_t, u]
+    L.spt_seed_fill.restype = None
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != RT_OK:
+        msg = lib().rt_last_error()
+        raise RTError(rc, msg.decode() if msg else "rt error")
+    return rc
+
+
+def device_count():
+    n = lib().rt_device_count()
+    return max(n, 0)
+
+
+def set_device(dev):
+    check(lib().rt_set_device(int(dev)))

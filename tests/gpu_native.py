@@ -1,0 +1,37 @@
+"""ctypes driver for tests/native/libgpu_math_check.so (test infrastructure)."""
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+
+# (name, fn id, lo, hi) float-bit ranges: the hot path's input domains.
+DOMAINS = [
+    ("powf_y20", 0, 0x00000000, 0x40000000),     # raytracer.cpp:165, dot in (0, 2]
+    ("powf_gamma", 1, 0x00000000, 0x3f800000),   # vec.h:62, [0, 1]
+    ("powf_gamma_negzero", 1, 0x80000000, 0x80000000),
+    ("expf_all", 2, 0x00000000, 0xffffffff),     # raytracer.cpp:487-489
+    ("sinf", 3, 0x00000000, 0x41000000),         # geomfunc.h:66,262, [0, 8]
+    ("cosf", 4, 0x00000000, 0x41000000),         # geomfunc.h:65,261
+]
+
+
+def lib():
+    path = os.path.join(HERE, "libgpu_math_check.so")
+    if not os.path.exists(path):
+        subprocess.run(["make", "-s", "-C", HERE, "libgpu_math_check.so"], check=True)
+    L = C.CDLL(path)
+    L.gmc_run.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+    return L
+
+
+def math_check(domains=DOMAINS):
+    L = lib()
+    out = {}
+    for name, fn, lo, hi in domains:
+        bad, first = C.c_uint64(), C.c_uint32()
+        rc = L.gmc_run(fn, lo, hi, C.byref(bad), C.byref(first))
+        if rc != 0:
+            raise RuntimeError("gmc_run failed (%d) on %s" % (rc, name))
+        out[name] = (hi - lo + 1, bad.value, hex(first.value))
+    return out
