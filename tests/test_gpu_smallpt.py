@@ -59,3 +59,22 @@ def test_batching_is_exact(rt):
         a.render(1)
     b.render(4)
     assert (a.colors == b.colors).all() and (a.seeds == b.seeds).all() and (a.pixels == b.pixels).all()
+
+
+# Full BASELINE sizes, checked against golden hashes of the reference-built
+# core (tests/golden/known_answers.json, oracle/_ref): configs[2] and the bench
+# / configs[3] frames.
+@pytest.mark.parametrize("key", ["1024x768_64spp", "1920x1080_64spp", "1920x1080_256spp"])
+def test_full_size_golden(rt, oracle, key):
+    import json
+    import os
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
+    g = gold["smallpt"][key]
+    res, spp = key.split("_")
+    w, h = map(int, res.split("x"))
+    f = rt.SmallptFrame(w, h)
+    spp = int(spp[:-3])
+    f.render(spp // 2)            # two launches: also exercises the first_sample > 0 path
+    f.render(spp - spp // 2)
+    got = (oracle.fnv1a64(f.colors), oracle.fnv1a64(f.pixels), oracle.fnv1a64(f.seeds))
+    assert got == (g["colors"], g["pixels"], g["seeds"])

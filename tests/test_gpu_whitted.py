@@ -36,3 +36,13 @@ def test_ragged_sizes(rt, oracle, w, h):
     ref, rc = oracle.whitted_render(w, h, row_begin=20, row_end=h)
     got, gc = rt.whitted_render(w, h, row_begin=20, row_end=h, counters=True)
     assert (got == ref).all() and gc == rc
+
+
+def test_golden_hashes(rt, oracle):
+    import json
+    import os
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
+    for key, g in gold["whitted"].items():
+        w, h = map(int, key.split("x"))
+        f, c = rt.whitted_render(w, h, counters=True)
+        assert oracle.fnv1a64(f) == g["xrgb"] and c == g["counters"], key
