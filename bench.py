@@ -31,6 +31,7 @@ import torch  # noqa: E402  (torch first: one HIP runtime in the process)
 import torch.distributed as dist  # noqa: E402
 
 import rtamd  # noqa: E402
+from rtamd import dist as rdist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: peak FP32 vector
@@ -46,15 +47,6 @@ def parse():
     ap.add_argument("--no-whitted", action="store_true", help="skip the Whitted side line")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU sample length")
     return ap.parse_args()
-
-
-def band(rank, world):
-    """Contiguous row band [r0, r1) of rank `rank` (flipped-slot order so
-    the colour slots of rank k are the k-th contiguous chunk)."""
-    B = H // world
-    assert B * world == H, "H must divide by the GPU count"
-    r0 = H - (rank + 1) * B
-    return r0, r0 + B
 
 
 def cpu_baseline(args):
@@ -148,36 +140,30 @@ def main():
 
     spheres, ns = rtamd.scenes.cornell()
     cam = rtamd.scenes.cornell_camera(W, H)
-    d_spheres = torch.frombuffer(bytearray(bytes(spheres)), dtype=torch.uint8).to(dev)
+    scene = rtamd.SmallptScene(spheres, ns)       # uploaded once, SGPR geometry packed
     seeds0 = torch.from_numpy(rtamd.scenes.seeds(W, H).view(np.int32)).to(dev)  # pristine
     seeds = torch.empty_like(seeds0)
     colors = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
     pixels = torch.zeros(W * H, dtype=torch.int32, device=dev)
     cnt = torch.zeros(4, dtype=torch.int64, device=dev)
-    r0, r1 = band(rank, world)
+    r0, r1 = rdist.row_band(rank, world, H)
     B = r1 - r0
     s = torch.cuda.current_stream(dev)
-    if distributed:
-        col_parts = list(colors.view(world, 3 * B * W).unbind(0))       # flipped slots: rank k = chunk k
-        px_parts = [pixels[(H - (k + 1) * B) * W:(H - k * B) * W] for k in range(world)]
-        my_col = colors[(H - r1) * W * 3:(H - r0) * W * 3]
-        my_px = pixels[r0 * W:r1 * W]
+    gather = rdist.FrameGather(colors, pixels, rank, world, W, H)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
 
     def step(i=None, counters=None):
         if i is not None:
             ev[i][0].record(s)
-        rtamd.check(L.spt_render_async(d_spheres.data_ptr(), ns, C.byref(cam), colors.data_ptr(),
+        rtamd.check(L.spt_scene_render_async(scene.handle, C.byref(cam), colors.data_ptr(),
                                        seeds0.data_ptr(), seeds.data_ptr(), pixels.data_ptr(), W, H, r0, r1,
                                        0, SPP, rtamd.SPT_PATH_TRACING,
                                        counters.data_ptr() if counters is not None else None,
                                        s.cuda_stream))
         if i is not None:
             ev[i][1].record(s)
-        if distributed:
-            dist.all_gather(col_parts, my_col.clone())
-            dist.all_gather(px_parts, my_px.clone())
+        gather.gather()          # RCCL all-gather of the HDR + RGBA8 bands (no-op at N=1)
 
     for _ in range(args.warmup):
         step()

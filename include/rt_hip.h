@@ -104,15 +104,30 @@ int spt_render(const rt_sphere *spheres, unsigned nspheres, const rt_camera *cam
                float *colors, uint32_t *seeds, uint32_t *pixels, int w, int h,
                int first_sample, int nsamples, int mode, uint64_t *counters);
 
-/* Asynchronous, device-resident, rows [row_begin,row_end) of the frame.
- * Buffers are full-frame device arrays laid out as above; seeds are read
- * from d_seeds_in and the advanced state written to d_seeds_out (may alias).
- * camera is read on the host at call time (passed by value to the kernel). */
+/* Device-resident buffers, rows [row_begin,row_end) of the frame.  Buffers
+ * are full-frame device arrays laid out as above; seeds are read from
+ * d_seeds_in and the advanced state written to d_seeds_out (may alias).
+ * camera is read on the host at call time (passed by value to the kernel).
+ * Reads the sphere array back once to prepare it and synchronises `stream`
+ * before returning; use spt_scene_* to stay fully asynchronous. */
 int spt_render_async(const rt_sphere *d_spheres, unsigned nspheres, const rt_camera *camera,
                      float *d_colors, const uint32_t *d_seeds_in, uint32_t *d_seeds_out,
                      uint32_t *d_pixels, int w, int h, int row_begin, int row_end,
                      int first_sample, int nsamples, int mode, uint64_t *d_counters,
                      void *stream);
+
+/* Prepared scene: uploads the sphere array once (device AoS + SoA + light
+ * list) and keeps the kernel-argument copy of the geometry that the
+ * size-specialised kernels hold in SGPRs.  Reuse it across frames. */
+typedef struct spt_scene spt_scene;
+int spt_scene_create(const rt_sphere *spheres, unsigned nspheres, spt_scene **out);
+int spt_scene_destroy(spt_scene *scene);
+/* spt_render_async on a prepared scene: no host<->device traffic, fully
+ * asynchronous on `stream` (graph-capturable). */
+int spt_scene_render_async(const spt_scene *scene, const rt_camera *camera, float *d_colors,
+                           const uint32_t *d_seeds_in, uint32_t *d_seeds_out, uint32_t *d_pixels,
+                           int w, int h, int row_begin, int row_end, int first_sample, int nsamples,
+                           int mode, uint64_t *d_counters, void *stream);
 
 /* Host helper: AllocateBuffers' seed fill (smallptGPU.cpp:105-110) --
  * srand(seed); seeds[i] = max(rand(), 2) for i < n, with the host libc's

@@ -253,6 +253,44 @@ RTM_HD float cosf(float x)
     return sincos_poly_eval(xr * sincos_sign(n & 3), xr * xr, sincos_tab((n & 2) != 0), n ^ 1);
 }
 
+// Branch-free sinf and cosf of one argument, |x| < 120, bit-identical to the
+// two glibc calls above (checked exhaustively by the same tests):
+//  * for |x| < pi/4 reduce_fast yields n = 0 and xr = x exactly, so the
+//    "small" path of sinf/cosf is the n = 0 case of the reduced path;
+//  * __sincosf_table[1] is table[0] with the cosine coefficients negated, and
+//    RN(-a*b - c) = -RN(a*b + c), so its cosine polynomial is the exact
+//    negation of table[0]'s;
+//  * |x| < 2^-12 returns x / 1.0f as glibc's tiny path does.
+// One reduction and both polynomials are evaluated for every lane: no
+// divergent branches in the wave.
+RTM_HD void sincosf(float x, float &sn, float &cs)
+{
+    const double xd = (double)x;
+    const uint32_t abstop = (f2u(x) >> 20) & 0x7ff;
+    int n;
+    const double xr = sincos_reduce(xd, n);
+    const double sg = ((n & 3) == 0 || (n & 3) == 3) ? 1.0 : -1.0;
+    const double xs = xr * sg, s = xr * xr;
+    // sine polynomial (coefficients common to both tables)
+    const double s1 = fma_d(s, -0x1.994eb3774cf24p-13, 0x1.1107605230bc4p-7);
+    const double x3 = s * xs;
+    const double x7 = s * x3;
+    const double ss = fma_d(x3, -0x1.555545995a603p-3, xs);
+    const float ps = (float)fma_d(s1, x7, ss);
+    // cosine polynomial of table[0]
+    const double x4 = s * s;
+    const double c1 = fma_d(s, -0x1.ffffffd0c621cp-2, 0x1.0000000000000p+0);
+    const double c2 = fma_d(s, 0x1.99343027bf8c3p-16, -0x1.6c087e89a359dp-10);
+    const double x6 = s * x4;
+    const double c = fma_d(x4, 0x1.55553e1068f19p-5, c1);
+    float pc = (float)fma_d(c2, x6, c);
+    if (n & 2) pc = -pc;
+    const bool odd = (n & 1) != 0;
+    sn = odd ? pc : ps;
+    cs = odd ? ps : pc;
+    if (abstop < 0x398) { sn = x; cs = 1.0f; }
+}
+
 }  // namespace rtm
 
 #endif

@@ -56,22 +56,40 @@ __device__ __forceinline__ v3 vxcross(v3 a, v3 b)
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 
-// SphereIntersect, geomfunc.h:32-59 (g = centre.xyz, rad*rad).
+// SphereIntersect, geomfunc.h:32-59 (g = centre.xyz, rad*rad), branch-free:
+// the square root of max(det, 0) is taken for every lane and a negative det
+// selects 0 afterwards -- the same float operations on every path the
+// reference takes, no divergent branch (NaN det also yields 0, as in the
+// reference).
 __device__ __forceinline__ float sphere_hit(float4 g, const ray3 &r)
 {
     const float opx = g.x - r.o.x, opy = g.y - r.o.y, opz = g.z - r.o.z;
     const float b = opx * r.d.x + opy * r.d.y + opz * r.d.z;
-    float det = b * b - (opx * opx + opy * opy + opz * opz) + g.w;
-    if (det < 0.f) return 0.f;
-    det = sqrtf(det);
-    float t = b - det;
-    if (t > EPS) return t;
-    t = b + det;
-    return t > EPS ? t : 0.f;
+    const float det = b * b - (opx * opx + opy * opy + opz * opz) + g.w;
+    const float sd = sqrtf(det < 0.f ? 0.f : det);
+    const float t1 = b - sd, t2 = b + sd;
+    const float t = t1 > EPS ? t1 : (t2 > EPS ? t2 : 0.f);
+    return det < 0.f ? 0.f : t;
 }
 
+// Sphere geometry sources for the nearest-hit / any-hit loops.
+//   FixGeo<N>: compile-time sphere count, passed by value as a kernel argument
+//              -> lives in SGPRs, loops fully unrolled (Cornell: N = 9);
+//   DynGeo   : runtime count, LDS (or global) float4 array.
+template <int N> struct FixGeo {
+    float4 g[N];
+    __device__ __forceinline__ constexpr int count() const { return N; }
+    __device__ __forceinline__ float4 at(int i) const { return g[i]; }
+};
+struct DynGeo {
+    const float4 *g;
+    int n;
+    __device__ __forceinline__ int count() const { return n; }
+    __device__ __forceinline__ float4 at(int i) const { return g[i]; }
+};
+
 struct Scene {                // per-block LDS copy (or global view for big scenes)
-    const float4 *geo;        // centre, rad^2
+    const float4 *geo;        // centre, rad^2 (per-lane lookups of the hit sphere)
     const float4 *emi;        // emission.xyz, refl (as int bits)
     const float4 *col;        // colour.xyz, rad
     const int *lights;        // indices with !viszero(e), ascending
@@ -79,35 +97,46 @@ struct Scene {                // per-block LDS copy (or global view for big scen
 };
 
 // Intersect, geomfunc.h:71-92: i descending, update iff d != 0 && d < t.
-__device__ __forceinline__ bool intersect(const Scene &S, const ray3 &r, float &t, int &id)
+template <class G>
+__device__ __forceinline__ bool intersect(const G &geo, const ray3 &r, float &t, int &id)
 {
     const float inf = 1e20f;
     t = inf;
     id = 0;
-    for (int i = S.n - 1; i >= 0; i--) {
-        const float d = sphere_hit(S.geo[i], r);
-        if ((d != 0.f) && (d < t)) { t = d; id = i; }
+#pragma unroll
+    for (int i = geo.count() - 1; i >= 0; i--) {
+        const float d = sphere_hit(geo.at(i), r);
+        const bool take = (d != 0.f) && (d < t);
+        t = take ? d : t;
+        id = take ? i : id;
     }
     return t < inf;
 }
 
-// IntersectP, geomfunc.h:94-110 (returns tests performed through ntests).
-__device__ __forceinline__ bool intersect_p(const Scene &S, const ray3 &r, float maxt, unsigned &ntests)
+// IntersectP, geomfunc.h:94-110.  All spheres are tested (no divergent early
+// exit); the result and the reference's test count (spheres tested down to and
+// including the first hit in descending order) are recovered from the highest
+// qualifying index.
+template <class G>
+__device__ __forceinline__ bool intersect_p(const G &geo, const ray3 &r, float maxt, unsigned &ntests)
 {
-    for (int i = S.n - 1; i >= 0; i--) {
-        ntests++;
-        const float d = sphere_hit(S.geo[i], r);
-        if ((d != 0.f) && (d < maxt)) return true;
+    int first = -1;
+#pragma unroll
+    for (int i = geo.count() - 1; i >= 0; i--) {
+        const float d = sphere_hit(geo.at(i), r);
+        first = (first < 0 && (d != 0.f) && (d < maxt)) ? i : first;
     }
-    return false;
+    ntests += first >= 0 ? (unsigned)(geo.count() - first) : (unsigned)geo.count();
+    return first >= 0;
 }
 
 struct Counts { unsigned long long isect, isectp, tests, samples; };
 
 // SampleLights, geomfunc.h:112-165.  UniformSampleSphere's two GetRandom()
 // arguments are drawn second-first, as the g++-built oracle does (:138).
-__device__ __forceinline__ v3 sample_lights(const Scene &S, uint32_t &s0, uint32_t &s1, v3 hit,
-                                            v3 nl, Counts &cnt)
+template <class G>
+__device__ __forceinline__ v3 sample_lights(const G &geo, const Scene &S, uint32_t &s0, uint32_t &s1,
+                                            v3 hit, v3 nl, Counts &cnt)
 {
     v3 result = mk(0.f, 0.f, 0.f);
     for (int li = 0; li < S.nlights; li++) {
@@ -123,7 +152,9 @@ __device__ __forceinline__ v3 sample_lights(const Scene &S, uint32_t &s0, uint32
         const float q = 1.f - zz * zz;
         const float rr = sqrtf((0.f > q) ? 0.f : q);
         const float phi = 2.f * PI_F * u2;
-        const v3 unit = mk(rr * rtm::cosf(phi), rr * rtm::sinf(phi), zz);
+        float sp_sin, sp_cos;
+        rtm::sincosf(phi, sp_sin, sp_cos);
+        const v3 unit = mk(rr * sp_cos, rr * sp_sin, zz);
         v3 sp = vsmul(rad, unit);
         sp = vadd(sp, mk(lg.x, lg.y, lg.z));
         ray3 sh;
@@ -138,7 +169,7 @@ __device__ __forceinline__ v3 sample_lights(const Scene &S, uint32_t &s0, uint32
         if (wi > 0.f) {
             unsigned nt = 0;
             cnt.isectp++;
-            const bool occluded = intersect_p(S, sh, len - EPS, nt);
+            const bool occluded = intersect_p(geo, sh, len - EPS, nt);
             cnt.tests += nt;
             if (!occluded) {
                 const float s = (4.f * PI_F * rad * rad) * wi * wo / (len * len);
@@ -156,9 +187,10 @@ __device__ __forceinline__ int to_int(float x)
     return (int)(rtm::powf(c, 1.f / 2.2f) * 255.f + .5f);
 }
 
-template <bool DL, bool COUNT, bool LDS>
+template <int FIXN, bool DL, bool COUNT, bool LDS>
 __global__ void __launch_bounds__(256)
-render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
+render_kernel(FixGeo<(FIXN > 0 ? FIXN : 1)> fgeo, const rt_sphere *__restrict__ spheres, int nspheres,
+              rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,
               uint32_t *seeds_out, uint32_t *__restrict__ pixels, int w, int h,
               int row_begin, int row_end, int first_sample, int nsamples,
@@ -195,6 +227,12 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         S.geo = g_geo; S.emi = g_emi; S.col = g_col; S.lights = g_lights; S.nlights = g_nlights;
     }
     S.n = nspheres;
+    // Nearest-hit / any-hit geometry: SGPR-resident kernel argument when the
+    // scene size was specialised at compile time, else the LDS/global array.
+    const auto geo = [&]() {
+        if constexpr (FIXN > 0) return fgeo;
+        else return DynGeo{S.geo, S.n};
+    }();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
@@ -242,7 +280,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 int id;
                 cnt.isect++;
                 cnt.tests += S.n;
-                if (!intersect(S, ray, t, id)) {
+                if (!intersect(geo, ray, t, id)) {
                     done = true;
                 } else {
                     const float4 og = S.geo[id], oe = S.emi[id], oc = S.col[id];
@@ -264,7 +302,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     } else if (refl == DIFF) {
                         specular = false;
                         thr = vmul(thr, mk(oc.x, oc.y, oc.z));
-                        v3 ld = sample_lights(S, s0, s1, hit, nl, cnt);
+                        v3 ld = sample_lights(geo, S, s0, s1, hit, nl, cnt);
                         ld = vmul(thr, ld);
                         rad = vadd(rad, ld);
                         if (DL) {
@@ -277,8 +315,10 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                             const v3 a = (fabsf(wv.x) > .1f) ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
                             v3 u = vnorm(vxcross(a, wv));
                             v3 v = vxcross(wv, u);
-                            u = vsmul(rtm::cosf(r1) * r2s, u);
-                            v = vsmul(rtm::sinf(r1) * r2s, v);
+                            float sn1, cs1;
+                            rtm::sincosf(r1, sn1, cs1);
+                            u = vsmul(cs1 * r2s, u);
+                            v = vsmul(sn1 * r2s, v);
                             v3 nd = vadd(u, v);
                             nd = vadd(nd, vsmul(sqrtf(1 - r2), wv));
                             ray.o = hit;
@@ -366,104 +406,191 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     }
 }
 
-// Global-memory SoA of the scene for scenes above MAXS_LDS.
-__global__ void prepare_kernel(const rt_sphere *__restrict__ spheres, int n, float4 *geo, float4 *emi,
-                               float4 *col, int *lights, int *nlights)
-{
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const rt_sphere &q = spheres[i];
-        geo[i] = make_float4(q.p.x, q.p.y, q.p.z, q.rad * q.rad);
-        emi[i] = make_float4(q.e.x, q.e.y, q.e.z, __int_as_float(q.refl));
-        col[i] = make_float4(q.c.x, q.c.y, q.c.z, q.rad);
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        int nl = 0;
-        for (int i = 0; i < n; i++) {
-            const rt_sphere &q = spheres[i];
-            if (!((q.e.x == 0.f) && (q.e.x == 0.f) && (q.e.z == 0.f))) lights[nl++] = i;
-        }
-        *nlights = nl;
-    }
-}
-
 }  // namespace smallpt
 }  // namespace rt
 
 // ------------------------------------------------------------------ host side
+#include <string.h>
+#include <vector>
 #include "rt_runtime.h"
+
+// A prepared scene (spt_scene_create): device AoS copy for the per-block LDS
+// staging, device SoA + light list for scenes above the LDS budget, and the
+// kernel-argument geometry for compile-time-specialised sizes.
+struct spt_scene {
+    int device = -1;
+    int n = 0;
+    rt_sphere *d_spheres = nullptr;   // n x 44 B
+    float4 *d_soa = nullptr;          // geo | emi | col (n each), then lights (int)
+    int nlights = 0;
+    std::vector<rt_sphere> host;
+};
 
 namespace {
 
-template <bool DL, bool COUNT, bool LDS>
-void launch(dim3 grid, hipStream_t s, const rt_sphere *d_spheres, int n, const rt_camera &cam,
-            float *colors, const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h,
-            int r0, int r1, int first, int ns, const float4 *gg, const float4 *ge, const float4 *gc,
-            const int *gl, int gnl, unsigned long long *cnt)
+constexpr int FIXN_CORNELL = 9;   // CornellSpheres (scene.h:29-40)
+
+template <int FIXN, bool DL, bool COUNT, bool LDS>
+void launch(dim3 grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam, float *colors,
+            const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h, int r0, int r1,
+            int first, int ns, unsigned long long *cnt)
 {
+    constexpr int FN = FIXN > 0 ? FIXN : 1;
+    rt::smallpt::FixGeo<FN> fg;
+    for (int i = 0; i < FN; i++) fg.g[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (FIXN > 0)   // centre, rad*rad: the float product SphereIntersect forms (geomfunc.h:42)
+        for (int i = 0; i < FIXN; i++) {
+            const rt_sphere &q = sc.host[i];
+            fg.g[i] = make_float4(q.p.x, q.p.y, q.p.z, q.rad * q.rad);
+        }
+    const int n = sc.n;
+    const float4 *gg = nullptr, *ge = nullptr, *gc = nullptr;
+    const int *gl = nullptr;
+    if (!LDS) {
+        gg = sc.d_soa; ge = gg + n; gc = ge + n;
+        gl = (const int *)(gc + n);
+    }
     const size_t lds = LDS ? (size_t)n * 3 * sizeof(float4) + (size_t)(n + 1) * sizeof(int) : 0;
-    hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, LDS>), grid, dim3(256), lds, s, d_spheres,
-                       n, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, gg, ge, gc, gl, gnl,
-                       cnt);
+    hipLaunchKernelGGL((rt::smallpt::render_kernel<FIXN, DL, COUNT, LDS>), grid, dim3(256), lds, s, fg,
+                       sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, gg, ge,
+                       gc, gl, sc.nlights, cnt);
+}
+
+template <int FIXN, bool LDS>
+void launch_mode(bool dl, bool count, dim3 grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam,
+                 float *colors, const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h,
+                 int r0, int r1, int first, int ns, unsigned long long *cnt)
+{
+    if (dl) {
+        if (count) launch<FIXN, true, true, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+        else launch<FIXN, true, false, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+    } else {
+        if (count) launch<FIXN, false, true, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+        else launch<FIXN, false, false, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+    }
+}
+
+int check_render_args(const rt_camera *camera, float *d_colors, const uint32_t *d_seeds_in,
+                      uint32_t *d_seeds_out, uint32_t *d_pixels, int w, int h, int row_begin, int row_end,
+                      int first_sample, int nsamples, int mode)
+{
+    if (!camera || !d_colors || !d_seeds_in || !d_seeds_out || !d_pixels)
+        return rtrt::fail(RT_ERR_INVALID, "spt render: null pointer");
+    if (w < 1 || h < 1 || first_sample < 0 || nsamples < 0)
+        return rtrt::fail(RT_ERR_INVALID, "spt render: bad sizes");
+    if (row_begin < 0 || row_end > h || row_begin > row_end)
+        return rtrt::fail(RT_ERR_INVALID, "spt render: bad row range");
+    if (mode != SPT_PATH_TRACING && mode != SPT_DIRECT_LIGHTING)
+        return rtrt::fail(RT_ERR_INVALID, "spt render: bad mode");
+    return RT_OK;
 }
 
 }  // namespace
 
+extern "C" int spt_scene_create(const rt_sphere *spheres, unsigned nspheres, spt_scene **out)
+{
+    if (!spheres || !out || nspheres < 1 || nspheres > (1u << 24))
+        return rtrt::fail(RT_ERR_INVALID, "spt_scene_create: bad arguments");
+    rtrt::DeviceState *st;
+    int rc = rtrt::state(&st);
+    if (rc) return rc;
+    spt_scene *sc = new spt_scene();
+    sc->device = st->device;
+    sc->n = (int)nspheres;
+    sc->host.assign(spheres, spheres + nspheres);
+    const int n = sc->n;
+    std::vector<float4> soa((size_t)3 * n + (n + 3) / 4);
+    int *lights = (int *)(soa.data() + 3 * (size_t)n);
+    for (int i = 0; i < n; i++) {
+        const rt_sphere &q = spheres[i];
+        soa[i] = make_float4(q.p.x, q.p.y, q.p.z, q.rad * q.rad);
+        int refl = q.refl;
+        float frefl;
+        memcpy(&frefl, &refl, 4);
+        soa[n + i] = make_float4(q.e.x, q.e.y, q.e.z, frefl);
+        soa[2 * (size_t)n + i] = make_float4(q.c.x, q.c.y, q.c.z, q.rad);
+        if (!((q.e.x == 0.f) && (q.e.x == 0.f) && (q.e.z == 0.f))) lights[sc->nlights++] = i;  // vec.h:44
+    }
+    hipError_t e = hipMalloc(&sc->d_spheres, sizeof(rt_sphere) * n);
+    if (e == hipSuccess) e = hipMalloc(&sc->d_soa, sizeof(float4) * soa.size());
+    if (e == hipSuccess) e = hipMemcpy(sc->d_spheres, spheres, sizeof(rt_sphere) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(sc->d_soa, soa.data(), sizeof(float4) * soa.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (sc->d_spheres) (void)hipFree(sc->d_spheres);
+        if (sc->d_soa) (void)hipFree(sc->d_soa);
+        delete sc;
+        return rtrt::fail_hip(e, "spt_scene_create upload");
+    }
+    *out = sc;
+    return RT_OK;
+}
+
+extern "C" int spt_scene_destroy(spt_scene *sc)
+{
+    if (!sc) return RT_OK;
+    (void)hipSetDevice(sc->device);
+    (void)hipDeviceSynchronize();
+    if (sc->d_spheres) (void)hipFree(sc->d_spheres);
+    if (sc->d_soa) (void)hipFree(sc->d_soa);
+    delete sc;
+    return RT_OK;
+}
+
+extern "C" int spt_scene_render_async(const spt_scene *sc, const rt_camera *camera, float *d_colors,
+                                      const uint32_t *d_seeds_in, uint32_t *d_seeds_out, uint32_t *d_pixels,
+                                      int w, int h, int row_begin, int row_end, int first_sample,
+                                      int nsamples, int mode, uint64_t *d_counters, void *stream)
+{
+    if (!sc) return rtrt::fail(RT_ERR_INVALID, "spt_scene_render_async: null scene");
+    int rc = check_render_args(camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, row_begin,
+                               row_end, first_sample, nsamples, mode);
+    if (rc) return rc;
+    if (row_begin == row_end) return RT_OK;
+    dim3 grid((w + 15) / 16, (row_end - row_begin + 15) / 16);
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long *cnt = (unsigned long long *)d_counters;
+    const bool dl = mode == SPT_DIRECT_LIGHTING;
+    if (sc->n == FIXN_CORNELL)
+        launch_mode<FIXN_CORNELL, true>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in,
+                                        d_seeds_out, d_pixels, w, h, row_begin, row_end, first_sample,
+                                        nsamples, cnt);
+    else if (sc->n <= rt::smallpt::MAXS_LDS)
+        launch_mode<0, true>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
+                             d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
+    else
+        launch_mode<0, false>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
+                              d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
+    return rtrt::check_launch("spt render_kernel");
+}
+
+// Device-pointer-only entry: stages the spheres through a cached scene
+// object (one D2H read of the sphere array per new pointer/size).
 extern "C" int spt_render_async(const rt_sphere *d_spheres, unsigned nspheres, const rt_camera *camera,
                                 float *d_colors, const uint32_t *d_seeds_in, uint32_t *d_seeds_out,
                                 uint32_t *d_pixels, int w, int h, int row_begin, int row_end,
                                 int first_sample, int nsamples, int mode, uint64_t *d_counters,
                                 void *stream)
 {
-    if (!d_spheres || !camera || !d_colors || !d_seeds_in || !d_seeds_out || !d_pixels)
-        return rtrt::fail(RT_ERR_INVALID, "spt_render_async: null pointer");
-    if (nspheres < 1 || nspheres > (1u << 24) || w < 1 || h < 1 || first_sample < 0 || nsamples < 0)
-        return rtrt::fail(RT_ERR_INVALID, "spt_render_async: bad sizes");
-    if (row_begin < 0 || row_end > h || row_begin > row_end)
-        return rtrt::fail(RT_ERR_INVALID, "spt_render_async: bad row range");
-    if (mode != SPT_PATH_TRACING && mode != SPT_DIRECT_LIGHTING)
-        return rtrt::fail(RT_ERR_INVALID, "spt_render_async: bad mode");
-    if (row_begin == row_end) return RT_OK;
-    rtrt::DeviceState *st;
-    int rc = rtrt::state(&st);
+    if (!d_spheres || nspheres < 1 || nspheres > (1u << 24))
+        return rtrt::fail(RT_ERR_INVALID, "spt_render_async: bad scene");
+    int rc = check_render_args(camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, row_begin,
+                               row_end, first_sample, nsamples, mode);
     if (rc) return rc;
-    hipStream_t s = (hipStream_t)stream;
-    const int n = (int)nspheres;
-    const bool lds = n <= rt::smallpt::MAXS_LDS;
-    const float4 *gg = nullptr, *ge = nullptr, *gc = nullptr;
-    const int *gl = nullptr;
-    int gnl = 0;
-    if (!lds) {
-        // Large scene: SoA copy in global memory (slot 6), light count read back once.
-        void *buf;
-        const size_t bytes = (size_t)n * (3 * sizeof(float4) + sizeof(int)) + 16;
-        if ((rc = rtrt::scratch(*st, 6, bytes, &buf))) return rc;
-        float4 *geo = (float4 *)buf, *emi = geo + n, *col = emi + n;
-        int *lights = (int *)(col + n);
-        int *nl = lights + n;
-        hipLaunchKernelGGL(rt::smallpt::prepare_kernel, dim3(64), dim3(256), 0, s, d_spheres, n, geo, emi,
-                           col, lights, nl);
-        if ((rc = rtrt::check_launch("spt prepare_kernel"))) return rc;
-        hipError_t e = hipMemcpyAsync(&gnl, nl, sizeof(int), hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return rtrt::fail_hip(e, "spt light count");
-        gg = geo; ge = emi; gc = col; gl = lights;
+    std::vector<rt_sphere> host(nspheres);
+    hipError_t e = hipMemcpyAsync(host.data(), d_spheres, sizeof(rt_sphere) * nspheres, hipMemcpyDeviceToHost,
+                                  (hipStream_t)stream);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "spt_render_async scene read");
+    spt_scene *sc;
+    if ((rc = spt_scene_create(host.data(), nspheres, &sc))) return rc;
+    rc = spt_scene_render_async(sc, camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, row_begin,
+                                row_end, first_sample, nsamples, mode, d_counters, stream);
+    if (rc == RT_OK) {
+        e = hipStreamSynchronize((hipStream_t)stream);
+        if (e != hipSuccess) rc = rtrt::fail_hip(e, "spt_render_async");
     }
-    dim3 grid((w + 15) / 16, (row_end - row_begin + 15) / 16);
-    unsigned long long *cnt = (unsigned long long *)d_counters;
-    const rt_camera &cam = *camera;
-#define RT_SPT_LAUNCH(DL, C, L)                                                                        \
-    launch<DL, C, L>(grid, s, d_spheres, n, cam, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h,   \
-                     row_begin, row_end, first_sample, nsamples, gg, ge, gc, gl, gnl, cnt)
-    const bool dl = mode == SPT_DIRECT_LIGHTING;
-    if (lds) {
-        if (dl) { if (cnt) RT_SPT_LAUNCH(true, true, true); else RT_SPT_LAUNCH(true, false, true); }
-        else    { if (cnt) RT_SPT_LAUNCH(false, true, true); else RT_SPT_LAUNCH(false, false, true); }
-    } else {
-        if (dl) { if (cnt) RT_SPT_LAUNCH(true, true, false); else RT_SPT_LAUNCH(true, false, false); }
-        else    { if (cnt) RT_SPT_LAUNCH(false, true, false); else RT_SPT_LAUNCH(false, false, false); }
-    }
-#undef RT_SPT_LAUNCH
-    return rtrt::check_launch("spt render_kernel");
+    spt_scene_destroy(sc);
+    return rc;
 }
 
 extern "C" int spt_render(const rt_sphere *spheres, unsigned nspheres, const rt_camera *camera,
@@ -476,23 +603,23 @@ extern "C" int spt_render(const rt_sphere *spheres, unsigned nspheres, const rt_
     int rc = rtrt::state(&st);
     if (rc) return rc;
     const size_t npx = (size_t)w * h;
-    void *d_s, *d_col, *d_seed, *d_px, *d_cnt;
-    if ((rc = rtrt::scratch(*st, 0, sizeof(rt_sphere) * nspheres, &d_s))) return rc;
+    void *d_col, *d_seed, *d_px, *d_cnt;
     if ((rc = rtrt::scratch(*st, 1, 3 * sizeof(float) * npx, &d_col))) return rc;
     if ((rc = rtrt::scratch(*st, 2, 2 * sizeof(uint32_t) * npx, &d_seed))) return rc;
     if ((rc = rtrt::scratch(*st, 3, sizeof(uint32_t) * npx, &d_px))) return rc;
     if ((rc = rtrt::scratch(*st, 4, 4 * sizeof(uint64_t), &d_cnt))) return rc;
+    spt_scene *sc;
+    if ((rc = spt_scene_create(spheres, nspheres, &sc))) return rc;
     hipStream_t s = st->stream;
-    hipError_t e = hipMemcpyAsync(d_s, spheres, sizeof(rt_sphere) * nspheres, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_seed, seeds, 2 * sizeof(uint32_t) * npx, hipMemcpyHostToDevice, s);
+    hipError_t e = hipMemcpyAsync(d_seed, seeds, 2 * sizeof(uint32_t) * npx, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && first_sample > 0)
         e = hipMemcpyAsync(d_col, colors, 3 * sizeof(float) * npx, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && counters) e = hipMemsetAsync(d_cnt, 0, 4 * sizeof(uint64_t), s);
-    if (e != hipSuccess) return rtrt::fail_hip(e, "spt_render H2D");
-    rc = spt_render_async((const rt_sphere *)d_s, nspheres, camera, (float *)d_col, (uint32_t *)d_seed,
-                          (uint32_t *)d_seed, (uint32_t *)d_px, w, h, 0, h, first_sample, nsamples, mode,
-                          counters ? (uint64_t *)d_cnt : nullptr, s);
-    if (rc) return rc;
+    if (e != hipSuccess) { spt_scene_destroy(sc); return rtrt::fail_hip(e, "spt_render H2D"); }
+    rc = spt_scene_render_async(sc, camera, (float *)d_col, (uint32_t *)d_seed, (uint32_t *)d_seed,
+                                (uint32_t *)d_px, w, h, 0, h, first_sample, nsamples, mode,
+                                counters ? (uint64_t *)d_cnt : nullptr, s);
+    if (rc) { spt_scene_destroy(sc); return rc; }
     e = hipMemcpyAsync(seeds, d_seed, 2 * sizeof(uint32_t) * npx, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess && nsamples > 0) {
         e = hipMemcpyAsync(colors, d_col, 3 * sizeof(float) * npx, hipMemcpyDeviceToHost, s);
@@ -501,6 +628,7 @@ extern "C" int spt_render(const rt_sphere *spheres, unsigned nspheres, const rt_
     if (e == hipSuccess && counters)
         e = hipMemcpyAsync(counters, d_cnt, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
+    spt_scene_destroy(sc);
     if (e != hipSuccess) return rtrt::fail_hip(e, "spt_render D2H");
     return RT_OK;
 }

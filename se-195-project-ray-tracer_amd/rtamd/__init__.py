@@ -18,7 +18,7 @@ from ._lib import (Camera, Primitive, RTError, Sphere, Vec3, check, device_count
                    set_device, SPT_DIRECT_LIGHTING, SPT_PATH_TRACING)
 
 __all__ = ["Camera", "Primitive", "Sphere", "Vec3", "RTError", "scenes", "lib", "check",
-           "device_count", "set_device", "whitted_render", "SmallptFrame",
+           "device_count", "set_device", "whitted_render", "SmallptFrame", "SmallptScene",
            "SPT_PATH_TRACING", "SPT_DIRECT_LIGHTING"]
 
 
@@ -68,3 +68,24 @@ class SmallptFrame:
         self.current_sample += nsamples
         self.counters = [a + b for a, b in zip(self.counters, cnt)]
         return self
+
+
+class SmallptScene:
+    """Prepared device scene (spt_scene_create); .handle is passed to
+    spt_scene_render_async.  Freed with close() / garbage collection."""
+
+    def __init__(self, spheres, nspheres):
+        self.handle = C.c_void_p()
+        check(lib().spt_scene_create(C.addressof(spheres), nspheres, C.byref(self.handle)))
+        self.n = nspheres
+
+    def close(self):
+        if self.handle:
+            lib().spt_scene_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

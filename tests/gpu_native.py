@@ -13,6 +13,10 @@ DOMAINS = [
     ("expf_all", 2, 0x00000000, 0xffffffff),     # raytracer.cpp:487-489
     ("sinf", 3, 0x00000000, 0x41000000),         # geomfunc.h:66,262, [0, 8]
     ("cosf", 4, 0x00000000, 0x41000000),         # geomfunc.h:65,261
+    ("sincosf_sin", 5, 0x00000000, 0x41000000),  # branch-free pair used by smallpt.hip
+    ("sincosf_cos", 6, 0x00000000, 0x41000000),
+    ("sincosf_sin_neg", 5, 0x80000000, 0xc1000000),
+    ("sincosf_cos_neg", 6, 0x80000000, 0xc1000000),
 ]
 
 

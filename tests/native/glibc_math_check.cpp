@@ -58,6 +58,14 @@ int main(int argc, char **argv)
         [](float x) { float s, c; ::sincosf(x, &s, &c); return s; });
     run("sincosf_cos", 0, trig_hi, [](float x) { return rtm::cosf(x); },
         [](float x) { float s, c; ::sincosf(x, &s, &c); return c; });
+    run("sincosf_branchless_sin", 0, trig_hi, [](float x) { float a, b; rtm::sincosf(x, a, b); return a; },
+        [](float x) { return ::sinf(x); });
+    run("sincosf_branchless_cos", 0, trig_hi, [](float x) { float a, b; rtm::sincosf(x, a, b); return b; },
+        [](float x) { return ::cosf(x); });
+    run("sincosf_branchless_sin_neg", 0x80000000u, 0x80000000u + trig_hi,
+        [](float x) { float a, b; rtm::sincosf(x, a, b); return a; }, [](float x) { return ::sinf(x); });
+    run("sincosf_branchless_cos_neg", 0x80000000u, 0x80000000u + trig_hi,
+        [](float x) { float a, b; rtm::sincosf(x, a, b); return b; }, [](float x) { return ::cosf(x); });
     // The exact smallpt domain: r1 = (2*PI) * (m * 2^-23), m < 2^23.
     {
         unsigned long long bad = 0;

@@ -16,7 +16,9 @@ __device__ __host__ inline float eval(int fn, float x)
     case 1: return rtm::powf(x, 1.f / 2.2f);
     case 2: return rtm::expf(x);
     case 3: return rtm::sinf(x);
-    default: return rtm::cosf(x);
+    case 4: return rtm::cosf(x);
+    case 5: { float a, b; rtm::sincosf(x, a, b); return a; }
+    default: { float a, b; rtm::sincosf(x, a, b); return b; }
     }
 }
 
@@ -26,7 +28,7 @@ static float host_glibc(int fn, float x)
     case 0: return ::powf(x, 20.0f);
     case 1: return ::powf(x, 1.f / 2.2f);
     case 2: return ::expf(x);
-    case 3: return ::sinf(x);
+    case 3: case 5: return ::sinf(x);
     default: return ::cosf(x);
     }
 }

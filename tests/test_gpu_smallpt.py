@@ -78,3 +78,68 @@ def test_full_size_golden(rt, oracle, key):
     f.render(spp - spp // 2)
     got = (oracle.fnv1a64(f.colors), oracle.fnv1a64(f.pixels), oracle.fnv1a64(f.seeds))
     assert got == (g["colors"], g["pixels"], g["seeds"])
+
+
+def _scene_arrays(rt, rows):
+    arr = (rt.Sphere * len(rows))()
+    for s, r in zip(arr, rows):
+        rt.scenes._sphere(s, *r)
+    return arr, len(rows)
+
+
+def test_generic_lds_path(rt, oracle):
+    """A 10-sphere scene (not the compile-time-specialised size 9) runs the
+    LDS loop path; must match the oracle bit for bit."""
+    rows = list(rt.scenes._CORNELL) + [(4.0, (20.0, 10.0, 100.0), (0, 0, 0), (.5, .9, .2), 1)]
+    spheres, n = _scene_arrays(rt, rows)
+    w, h = 128, 96
+    f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n)
+    f.render(3)
+    ref = _oracle_frame(oracle, w, h, [3], spheres=(spheres, n))
+    _check((f.colors, f.seeds, f.pixels, f.counters), ref)
+
+
+def test_large_scene_global_path(rt, oracle):
+    """configs[4] scene (10k spheres: above the LDS budget -> global SoA path)."""
+    spheres, n, cam = rt.scenes.complex10k()
+    w, h = 48, 32
+    rt.scenes.update_camera(cam, w, h)
+    f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n, camera=cam)
+    f.render(1)
+    ref = _oracle_frame(oracle, w, h, [1], spheres=(spheres, n), cam=cam)
+    _check((f.colors, f.seeds, f.pixels, f.counters), ref)
+
+
+def test_async_device_paths(rt, oracle):
+    """spt_scene_render_async and spt_render_async on device buffers, rows
+    split in two calls, seeds_in != seeds_out."""
+    import ctypes as C
+    import torch
+    w, h = 96, 64
+    S, n = rt.scenes.cornell()
+    cam = rt.scenes.cornell_camera(w, h)
+    dev = torch.device("cuda", 0)
+    seeds0 = torch.from_numpy(rt.scenes.seeds(w, h).view(np.int32)).to(dev)
+    outs = []
+    for use_scene in (True, False):
+        col = torch.zeros(3 * w * h, dtype=torch.float32, device=dev)
+        seeds = torch.zeros_like(seeds0)
+        px = torch.zeros(w * h, dtype=torch.int32, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        if use_scene:
+            sc = rt.SmallptScene(S, n)
+            for r0, r1 in ((0, 40), (40, h)):
+                rt.check(rt.lib().spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                                         seeds.data_ptr(), px.data_ptr(), w, h, r0, r1, 0, 2, 0,
+                                                         None, st))
+        else:
+            d_s = torch.frombuffer(bytearray(bytes(S)), dtype=torch.uint8).to(dev)
+            for r0, r1 in ((0, 40), (40, h)):
+                rt.check(rt.lib().spt_render_async(d_s.data_ptr(), n, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                                   seeds.data_ptr(), px.data_ptr(), w, h, r0, r1, 0, 2, 0, None, st))
+        torch.cuda.synchronize()
+        outs.append((col.cpu().numpy(), seeds.cpu().numpy().view(np.uint32), px.cpu().numpy().view(np.uint32)))
+    ref = _oracle_frame(oracle, w, h, [2])
+    for col, seeds, px in outs:
+        assert (col.view(np.uint32) == ref[0].view(np.uint32)).all()
+        assert (seeds == ref[1]).all() and (px == ref[2]).all()
