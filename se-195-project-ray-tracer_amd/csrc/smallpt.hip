@@ -410,6 +410,7 @@ render_kernel(FixGeo<(FIXN > 0 ? FIXN : 1)> fgeo, const rt_sphere *__restrict__ 
 }  // namespace rt
 
 // ------------------------------------------------------------------ host side
+#include <stdlib.h>
 #include <string.h>
 #include <vector>
 #include "rt_runtime.h"
@@ -550,7 +551,8 @@ extern "C" int spt_scene_render_async(const spt_scene *sc, const rt_camera *came
     hipStream_t s = (hipStream_t)stream;
     unsigned long long *cnt = (unsigned long long *)d_counters;
     const bool dl = mode == SPT_DIRECT_LIGHTING;
-    if (sc->n == FIXN_CORNELL)
+    static const bool no_fix = getenv("RT_SPT_NOFIX") != nullptr;   // A/B switch (tools/ab_smallpt.py)
+    if (sc->n == FIXN_CORNELL && !no_fix)
         launch_mode<FIXN_CORNELL, true>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in,
                                         d_seeds_out, d_pixels, w, h, row_begin, row_end, first_sample,
                                         nsamples, cnt);

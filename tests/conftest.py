@@ -3,6 +3,14 @@ import sys
 
 import pytest
 
+# torch bundles its own libamdhip64.so.7; if librt_hip.so is loaded first the
+# process binds /opt/rocm's copy and torch then finds no GPU.  Load torch's
+# runtime first so both share it (bench.py does the same).
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "se-195-project-ray-tracer_amd")
 for p in (PKG, os.path.join(ROOT, "tests"), ROOT):

@@ -60,7 +60,7 @@ def lib():
         L.ors_seeds_init.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
         L.ors_get_random.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ors_get_random.restype = C.c_float
-        L.ors_render.argtypes = [C.POINTER(Sphere), C.c_uint, C.POINTER(Camera), C.c_void_p,
+        L.ors_render.argtypes = [C.c_void_p, C.c_uint, C.c_void_p, C.c_void_p,
                                  C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_int, C.c_int, C.c_int, _u64p, C.c_int]
         L.ors_hypersphere.argtypes = [C.POINTER(Sphere), C.c_int, C.c_double]
@@ -122,7 +122,7 @@ def smallpt_render(spheres, n, cam, colors, seeds_arr, pixels, w, h, first_sampl
     if row_end is None:
         row_end = h
     cnt = (C.c_uint64 * 4)()
-    lib().ors_render(spheres, n, C.byref(cam), colors.ctypes.data, seeds_arr.ctypes.data,
+    lib().ors_render(C.addressof(spheres), n, C.addressof(cam), colors.ctypes.data, seeds_arr.ctypes.data,
                      pixels.ctypes.data, w, h, row_begin, row_end, first_sample, nsamples, dl,
                      cnt, nthreads)
     return list(cnt)
