@@ -66,6 +66,9 @@ __device__ __forceinline__ float sphere_hit(float4 g, const ray3 &r)
     const float opx = g.x - r.o.x, opy = g.y - r.o.y, opz = g.z - r.o.z;
     const float b = opx * r.d.x + opy * r.d.y + opz * r.d.z;
     const float det = b * b - (opx * opx + opy * opy + opz * opz) + g.w;
+#ifdef RT_SPT_BRANCHY
+    if (det < 0.f) return 0.f;
+#endif
     const float sd = sqrtf(det < 0.f ? 0.f : det);
     const float t1 = b - sd, t2 = b + sd;
     const float t = t1 > EPS ? t1 : (t2 > EPS ? t2 : 0.f);
@@ -187,8 +190,11 @@ __device__ __forceinline__ int to_int(float x)
     return (int)(rtm::powf(c, 1.f / 2.2f) * 255.f + .5f);
 }
 
+#ifndef RT_SPT_MINWAVES
+#define RT_SPT_MINWAVES 1   // __launch_bounds__ min waves per SIMD (occupancy A/B builds)
+#endif
 template <int FIXN, bool DL, bool COUNT, bool LDS>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, RT_SPT_MINWAVES)
 render_kernel(FixGeo<(FIXN > 0 ? FIXN : 1)> fgeo, const rt_sphere *__restrict__ spheres, int nspheres,
               rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,

@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
+# RT_HIP_LIB overrides the library path (A/B builds of kernel variants).
+LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(PKG_DIR, "librt_hip.so")
 
 RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NODEVICE = 0, -1, -2, -3
 SPT_PATH_TRACING, SPT_DIRECT_LIGHTING = 0, 1

@@ -43,6 +43,9 @@ int main(int argc, char **argv)
     camera.orig = {50.f, 45.f, 205.6f};
     camera.target = {50.f, 45 - 0.042612f, (float)204.6};
     UpdateCamera();
+    // The HIP runtime may draw from rand() while it initialises; bring it up
+    // first so AllocateBuffers' seeds are the srand(1) stream the oracle uses.
+    if (rt_device_count() < 1) { fprintf(stderr, "no HIP device\n"); return 1; }
     srand(1);
     SetUpHIP();
     for (int i = 0; i < passes; i++) UpdateRenderingGPU();

@@ -39,7 +39,14 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
     print("%s %.3f %.3f" % (os.environ.get("VARIANT", "?"), min(ts), float(np.median(ts))), flush=True)
     sys.exit(0)
 
-variants = {"fixed9": {}, "dyn_lds": {"RT_SPT_NOFIX": "1"}}
+variants = {}
+libs = sorted(os.listdir(os.path.join(ROOT, "build_ab"))) if os.path.isdir(os.path.join(ROOT, "build_ab")) else []
+for lib_name in (os.environ.get("LIBS", ",".join(libs)).split(",") if libs else []):
+    path = os.path.join(ROOT, "build_ab", lib_name, "librt_hip.so")
+    variants[lib_name + "/fixed9"] = {"RT_HIP_LIB": path}
+    variants[lib_name + "/dyn"] = {"RT_HIP_LIB": path, "RT_SPT_NOFIX": "1"}
+if not variants:
+    variants = {"fixed9": {}, "dyn_lds": {"RT_SPT_NOFIX": "1"}}
 for rnd in range(int(os.environ.get("ROUNDS", "2"))):
     for name, env in variants.items():
         e = dict(os.environ, VARIANT=name, **env)
