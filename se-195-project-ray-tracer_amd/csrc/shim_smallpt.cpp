@@ -184,3 +184,6 @@ void SmallptHipReadColors(float *out)
     hipError_t e = hipMemcpy(out, d_colors, sizeof(float) * 3 * width * height, hipMemcpyDeviceToHost);
     if (e != hipSuccess) die_hip("Failed to read the HIP colour buffer", e);
 }
+
+// Test / tooling hook: the seeds AllocateBuffers drew (host copy, 2*W*H).
+const unsigned int *SmallptHipInitialSeeds() { return h_seeds; }

@@ -50,29 +50,25 @@ __device__ __forceinline__ v3 vsmul(float k, v3 b) { return mk(k * b.x, k * b.y,
 __device__ __forceinline__ v3 vadd(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ v3 vsub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ v3 vmul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ v3 vnorm(v3 v) { const float l = 1.f / sqrtf(vdot(v, v)); return vsmul(l, v); }
+__device__ __forceinline__ v3 vnorm(v3 v) { const float l = 1.f / sqrt_rn(vdot(v, v)); return vsmul(l, v); }
 __device__ __forceinline__ v3 vxcross(v3 a, v3 b)
 {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 
-// SphereIntersect, geomfunc.h:32-59 (g = centre.xyz, rad*rad), branch-free:
-// the square root of max(det, 0) is taken for every lane and a negative det
-// selects 0 afterwards -- the same float operations on every path the
-// reference takes, no divergent branch (NaN det also yields 0, as in the
-// reference).
+// SphereIntersect, geomfunc.h:32-59 (g = centre.xyz, rad*rad).  The early
+// return on det < 0 is kept as a branch: when no lane of the wave reaches the
+// sphere's line the square root is skipped (measured +8 % over a branch-free
+// select form).  NaN det yields 0, as in the reference.
 __device__ __forceinline__ float sphere_hit(float4 g, const ray3 &r)
 {
     const float opx = g.x - r.o.x, opy = g.y - r.o.y, opz = g.z - r.o.z;
     const float b = opx * r.d.x + opy * r.d.y + opz * r.d.z;
     const float det = b * b - (opx * opx + opy * opy + opz * opz) + g.w;
-#ifdef RT_SPT_BRANCHY
     if (det < 0.f) return 0.f;
-#endif
-    const float sd = sqrtf(det < 0.f ? 0.f : det);
+    const float sd = sqrt_rn(det);
     const float t1 = b - sd, t2 = b + sd;
-    const float t = t1 > EPS ? t1 : (t2 > EPS ? t2 : 0.f);
-    return det < 0.f ? 0.f : t;
+    return t1 > EPS ? t1 : (t2 > EPS ? t2 : 0.f);
 }
 
 // Sphere geometry sources for the nearest-hit / any-hit loops.
@@ -153,7 +149,7 @@ __device__ __forceinline__ v3 sample_lights(const G &geo, const Scene &S, uint32
         // UniformSampleSphere, geomfunc.h:61-69
         const float zz = 1.f - 2.f * u1;
         const float q = 1.f - zz * zz;
-        const float rr = sqrtf((0.f > q) ? 0.f : q);
+        const float rr = sqrt_rn((0.f > q) ? 0.f : q);
         const float phi = 2.f * PI_F * u2;
         float sp_sin, sp_cos;
         rtm::sincosf(phi, sp_sin, sp_cos);
@@ -163,7 +159,7 @@ __device__ __forceinline__ v3 sample_lights(const G &geo, const Scene &S, uint32
         ray3 sh;
         sh.o = hit;
         sh.d = vsub(sp, hit);
-        const float len = sqrtf(vdot(sh.d, sh.d));
+        const float len = sqrt_rn(vdot(sh.d, sh.d));
         sh.d = vsmul(1.f / len, sh.d);
         float wo = vdot(sh.d, unit);
         if (wo > 0.f) continue;
@@ -316,7 +312,7 @@ render_kernel(FixGeo<(FIXN > 0 ? FIXN : 1)> fgeo, const rt_sphere *__restrict__ 
                         } else {
                             const float r1 = 2.f * PI_F * get_random(s0, s1);
                             const float r2 = get_random(s0, s1);
-                            const float r2s = sqrtf(r2);
+                            const float r2s = sqrt_rn(r2);
                             const v3 wv = nl;
                             const v3 a = (fabsf(wv.x) > .1f) ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
                             v3 u = vnorm(vxcross(a, wv));
@@ -326,7 +322,7 @@ render_kernel(FixGeo<(FIXN > 0 ? FIXN : 1)> fgeo, const rt_sphere *__restrict__ 
                             u = vsmul(cs1 * r2s, u);
                             v = vsmul(sn1 * r2s, v);
                             v3 nd = vadd(u, v);
-                            nd = vadd(nd, vsmul(sqrtf(1 - r2), wv));
+                            nd = vadd(nd, vsmul(sqrt_rn(1 - r2), wv));
                             ray.o = hit;
                             ray.d = nd;
                         }
@@ -351,7 +347,7 @@ render_kernel(FixGeo<(FIXN > 0 ? FIXN : 1)> fgeo, const rt_sphere *__restrict__ 
                             ray.o = hit;
                             ray.d = nd;
                         } else {
-                            const float kk = (into ? 1.f : -1.f) * (ddn * nnt + sqrtf(cos2t));
+                            const float kk = (into ? 1.f : -1.f) * (ddn * nnt + sqrt_rn(cos2t));
                             const v3 nkk = vsmul(kk, normal);
                             v3 td = vsmul(nnt, ray.d);
                             td = vsub(td, nkk);

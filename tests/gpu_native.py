@@ -17,6 +17,8 @@ DOMAINS = [
     ("sincosf_cos", 6, 0x00000000, 0x41000000),
     ("sincosf_sin_neg", 5, 0x80000000, 0xc1000000),
     ("sincosf_cos_neg", 6, 0x80000000, 0xc1000000),
+    ("sqrt_rn_pos", 7, 0x00000000, 0x7fffffff),  # rt_common.h sqrt_rn: every non-negative float, NaNs
+    ("sqrt_rn_neg", 7, 0x80000000, 0x80000010),  # -0 and a few negatives (NaN results)
 ]
 
 

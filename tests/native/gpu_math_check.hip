@@ -8,6 +8,7 @@
 #include <thread>
 #include <vector>
 #include "rt_glibc_math.h"
+#include "rt_common.h"
 
 __device__ __host__ inline float eval(int fn, float x)
 {
@@ -18,8 +19,15 @@ __device__ __host__ inline float eval(int fn, float x)
     case 3: return rtm::sinf(x);
     case 4: return rtm::cosf(x);
     case 5: { float a, b; rtm::sincosf(x, a, b); return a; }
-    default: { float a, b; rtm::sincosf(x, a, b); return b; }
+    case 6: { float a, b; rtm::sincosf(x, a, b); return b; }
+    default: return 0.f;
     }
+}
+
+__device__ inline float eval_dev(int fn, float x)
+{
+    if (fn == 7) return rt::sqrt_rn(x);
+    return eval(fn, x);
 }
 
 static float host_glibc(int fn, float x)
@@ -29,6 +37,7 @@ static float host_glibc(int fn, float x)
     case 1: return ::powf(x, 1.f / 2.2f);
     case 2: return ::expf(x);
     case 3: case 5: return ::sinf(x);
+    case 7: return ::sqrtf(x);
     default: return ::cosf(x);
     }
 }
@@ -36,7 +45,7 @@ static float host_glibc(int fn, float x)
 __global__ void eval_kernel(int fn, uint32_t lo, uint32_t n, uint32_t *out)
 {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        out[i] = rtm::f2u(eval(fn, rtm::u2f(lo + i)));
+        out[i] = rtm::f2u(eval_dev(fn, rtm::u2f(lo + i)));
 }
 
 // Compares device results for the float bit patterns [lo, hi] with the host

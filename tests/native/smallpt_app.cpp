@@ -2,8 +2,8 @@
 // the idle loop (displayfunc.cpp:197-204 -> UpdateRenderingGPU) over the HIP
 // drop-in shim (csrc/shim_smallpt.cpp).  UpdateCamera is the oracle's
 // restatement (test infrastructure).  Runs argv[3] UpdateRenderingGPU calls
-// and writes pixels (W*H u32), the device HDR colours (3*W*H f32) and
-// currentSample to argv[4].
+// and writes pixels (W*H u32), the device HDR colours (3*W*H f32) the
+// initial seeds AllocateBuffers drew and currentSample to argv[4].
 #include <stdio.h>
 #include <stdlib.h>
 #include <sys/time.h>
@@ -23,6 +23,7 @@ void SetUpHIP();
 void UpdateRenderingGPU();
 void ReInitGPU(const int);
 void SmallptHipReadColors(float *out);
+const unsigned int *SmallptHipInitialSeeds();
 
 void UpdateCamera() { ors_update_camera((or_camera *)&camera, width, height); }
 double WallClockTime()
@@ -54,6 +55,7 @@ int main(int argc, char **argv)
     FILE *f = fopen(argv[4], "wb");
     fwrite(pixels, 4, (size_t)width * height, f);
     fwrite(col, 4, (size_t)3 * width * height, f);
+    fwrite(SmallptHipInitialSeeds(), 4, (size_t)2 * width * height, f);
     fwrite(&currentSample, 4, 1, f);
     fclose(f);
     fprintf(stderr, "%s", captionBuffer);

@@ -39,12 +39,14 @@ def test_smallpt_shim_matches_cpu_path(oracle, tmp_path):
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     raw = np.fromfile(out, dtype=np.uint32)
-    px, col, cur = raw[:w * h], raw[w * h:w * h * 4].view(np.float32), int(raw[-1])
+    px, col = raw[:w * h], raw[w * h:w * h * 4].view(np.float32)
+    seeds0, cur = raw[w * h * 4:w * h * 6].copy(), int(raw[-1])
     assert cur == passes                      # < 20 passes: one sample per UpdateRenderingGPU
+    assert (seeds0 >= 2).all()                # AllocateBuffers' clamp (smallptGPU.cpp:106-108)
     S, n = oracle.cornell()
     cam = oracle.cornell_camera(w, h)
     rc = np.zeros(3 * w * h, np.float32)
-    seeds = oracle.seeds(w, h)
+    seeds = seeds0.copy()
     rp = np.zeros(w * h, np.uint32)
     oracle.smallpt_render(S, n, cam, rc, seeds, rp, w, h, 0, cur, nthreads=8)
     assert (col.view(np.uint32) == rc.view(np.uint32)).all() and (px == rp).all()
