@@ -24,8 +24,9 @@ __device__ __forceinline__ v3 mk(float x, float y, float z) { v3 r; r.x = x; r.y
 // a 2^32 pre-scale for x < 2^-96 and a +-0/inf class select.  For x >= 2^-96,
 // x = +-0, +inf and NaN the fixup alone is exact (v_sqrt of 0 / inf / NaN
 // needs no correction and the residual tests leave it unchanged), so only
-// positive x below 2^-96 take the library path -- a divergent branch that is
-// never entered in practice.  Checked against sqrtf for every float on the
+// x below 2^-96 other than +-0 (tiny or negative) take the library path -- a
+// divergent branch the ray-trace path never enters (its arguments are sums of
+// squares or checked non-negative).  Checked against sqrtf for every float on the
 // device (tests/test_gpu_math.py).
 __device__ __forceinline__ float sqrt_rn(float x)
 {
@@ -36,7 +37,7 @@ __device__ __forceinline__ float sqrt_rn(float x)
     const float r_up = __builtin_fmaf(-s_up, s, x);
     s = (r_dn <= 0.f) ? s_dn : s;
     s = (r_up > 0.f) ? s_up : s;
-    if (x > 0.f && x < 0x1p-96f) s = sqrtf(x);
+    if (x < 0x1p-96f && x != 0.f) s = sqrtf(x);   // tiny or negative (v_sqrt flushes -denormals)
     return s;
 }
 

@@ -38,3 +38,15 @@ int mainGPU(int argc, char **argv)
     glutMainLoop();
     return 0;
 }
+
+int mainCPU(int argc, char **argv);     // smallptCPU.cpp:169
+extern int useGPU, useOpenCL;
+
+// main, smallptGPU.cpp:874-884 (lives in the file this shim replaces).
+int main(int argc, char **argv)
+{
+    useOpenCL = 1;
+    useGPU = 1;
+    if (useOpenCL) return mainGPU(argc, argv);
+    return mainCPU(argc, argv);
+}

@@ -18,7 +18,7 @@ DOMAINS = [
     ("sincosf_sin_neg", 5, 0x80000000, 0xc1000000),
     ("sincosf_cos_neg", 6, 0x80000000, 0xc1000000),
     ("sqrt_rn_pos", 7, 0x00000000, 0x7fffffff),  # rt_common.h sqrt_rn: every non-negative float, NaNs
-    ("sqrt_rn_neg", 7, 0x80000000, 0x80000010),  # -0 and a few negatives (NaN results)
+    ("sqrt_rn_neg", 7, 0x80000000, 0xffffffff),  # every negative float (NaN results, -0)
 ]
 
 
