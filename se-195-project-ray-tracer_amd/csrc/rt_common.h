@@ -19,26 +19,25 @@ struct ray3 { v3 o, d; };
 
 __device__ __forceinline__ v3 mk(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
 
-// Correctly rounded sqrtf.  hipcc's sqrtf expands to v_sqrt_f32 (<= 1 ulp)
-// plus a two-residual fixup (s -/+ 1 ulp against fma(-s', s, x)), wrapped in
-// a 2^32 pre-scale for x < 2^-96 and a +-0/inf class select.  For x >= 2^-96,
-// x = +-0, +inf and NaN the fixup alone is exact (v_sqrt of 0 / inf / NaN
-// needs no correction and the residual tests leave it unchanged), so only
-// x below 2^-96 other than +-0 (tiny or negative) take the library path -- a
-// divergent branch the ray-trace path never enters (its arguments are sums of
-// squares or checked non-negative).  Checked against sqrtf for every float on the
-// device (tests/test_gpu_math.py).
+// Correctly rounded sqrtf in 14 VALU ops.  hipcc's sqrtf (gfx950) is: 2^32
+// pre-scale of x < 2^-96, v_sqrt_f32 (<= 1 ulp), the two-residual fixup
+// (s -/+ 1 ulp tested with fma(-s', s, x)), 2^-16 post-scale, and a final
+// class select returning x itself for +-0 / +inf.  That last select is
+// redundant after the fixup (v_sqrt gives +-0 / +inf exactly and both residual
+// tests then leave it), so it is dropped; everything else is kept.  Checked
+// against sqrtf for all 2^32 inputs on the device (tests/test_gpu_math.py).
 __device__ __forceinline__ float sqrt_rn(float x)
 {
-    float s = __builtin_amdgcn_sqrtf(x);
+    const bool tiny = x < 0x1p-96f;
+    const float xs = tiny ? x * 0x1p32f : x;
+    float s = __builtin_amdgcn_sqrtf(xs);
     const float s_dn = __uint_as_float(__float_as_uint(s) - 1u);
     const float s_up = __uint_as_float(__float_as_uint(s) + 1u);
-    const float r_dn = __builtin_fmaf(-s_dn, s, x);
-    const float r_up = __builtin_fmaf(-s_up, s, x);
+    const float r_dn = __builtin_fmaf(-s_dn, s, xs);
+    const float r_up = __builtin_fmaf(-s_up, s, xs);
     s = (r_dn <= 0.f) ? s_dn : s;
     s = (r_up > 0.f) ? s_up : s;
-    if (x < 0x1p-96f && x != 0.f) s = sqrtf(x);   // tiny or negative (v_sqrt flushes -denormals)
-    return s;
+    return tiny ? s * 0x1p-16f : s;
 }
 
 // Wave-level u64 sum (64 lanes) used for the optional work counters.

@@ -39,6 +39,18 @@ constexpr float EPS = 0.001f;   // common.h:24
 constexpr int SPHERE = 1, PLANE = 2;
 
 struct Scene {
+    // Geometry in dense per-type arrays (no index indirection in the hot
+    // loops): the nearest-hit and occlusion results are independent of the
+    // visiting order once distance ties go to the lowest primitive index
+    // (the reference's strict '<' over ascending s, raytracer.cpp:39-49).
+    float4 sph[MAXP];   // sphere centre.xyz, SqRadius
+    float4 pln[MAXP];   // plane N.xyz, D
+    int sph_id[MAXP], pln_id[MAXP];        // original primitive index
+    float4 osph[MAXP];  // non-light spheres (occluders, raytracer.cpp:100)
+    float4 opln[MAXP];  // non-light planes
+    int osph_pos[MAXP], opln_pos[MAXP];    // position in the non-light order (test counts)
+    int ns, np, nos, nop;
+    // Per-primitive records for per-lane lookups of the hit primitive.
     float4 geo[MAXP];   // sphere: centre.xyz, SqRadius   plane: N.xyz, D
     float4 mat0[MAXP];  // colour.xyz, refl
     float4 mat1[MAXP];  // refr, diff, spec, rindex
@@ -46,41 +58,41 @@ struct Scene {
     float rrad[MAXP];   // RRadius (sphere normal scale)
     int type[MAXP];
     int light[MAXP];
-    int nonlight[MAXP]; // indices of m_Light == 0 primitives, in index order
     int lights[MAXP];   // indices of m_Light > 0 primitives, in index order
     int n, nnonlight, nlights;
 };
 
-// Primitive_Intersect, scene.cpp:125-190.  Returns HIT 1 / INPRIM -1 / MISS 0.
-__device__ __forceinline__ int intersect(int type, float4 g, const ray3 &r, float &dist)
+// Sphere half of Primitive_Intersect (scene.cpp:130-169): the candidate
+// distance (INPRIM: i2, HIT: i1) or +inf with res = 0.
+__device__ __forceinline__ float sphere_cand(float4 g, const ray3 &r, int &res)
 {
-    if (type == SPHERE) {
-        float vx = r.o.x - g.x, vy = r.o.y - g.y, vz = r.o.z - g.z;
-        float b = vx * r.d.x + vy * r.d.y + vz * r.d.z;
-        b = -b;
-        float det = (b * b) - (vx * vx + vy * vy + vz * vz) + g.w;
-        int ret = 0;
-        if (det > 0) {
-            det = sqrt_rn(det);
-            float i1 = b - det, i2 = b + det;
-            if (i2 > 0) {
-                if (i1 < 0) {
-                    if (i2 < dist) { dist = i2; ret = -1; }
-                } else if (i1 < dist) {
-                    dist = i1; ret = 1;
-                }
-            }
-        }
-        return ret;
-    }
-    if (type == PLANE) {
-        float d = g.x * r.d.x + g.y * r.d.y + g.z * r.d.z;
-        if (d != 0) {
-            float t = -((g.x * r.o.x + g.y * r.o.y + g.z * r.o.z) + g.w) / d;
-            if (t > 0 && t < dist) { dist = t; return 1; }
+    const float vx = r.o.x - g.x, vy = r.o.y - g.y, vz = r.o.z - g.z;
+    float b = vx * r.d.x + vy * r.d.y + vz * r.d.z;
+    b = -b;
+    float det = (b * b) - (vx * vx + vy * vy + vz * vz) + g.w;
+    res = 0;
+    float cand = __builtin_inff();
+    if (det > 0) {
+        det = sqrt_rn(det);
+        const float i1 = b - det, i2 = b + det;
+        if (i2 > 0) {
+            cand = i1 < 0 ? i2 : i1;
+            res = i1 < 0 ? -1 : 1;
         }
     }
-    return 0;
+    return cand;
+}
+
+// Plane half of Primitive_Intersect (scene.cpp:171-185).
+__device__ __forceinline__ float plane_cand(float4 g, const ray3 &r)
+{
+    const float d = g.x * r.d.x + g.y * r.d.y + g.z * r.d.z;
+    float cand = __builtin_inff();
+    if (d != 0) {
+        const float t = -((g.x * r.o.x + g.y * r.o.y + g.z * r.o.z) + g.w) / d;
+        if (t > 0) cand = t;
+    }
+    return cand;
 }
 
 // Primitive_GetNormal, scene.cpp:34-53.
@@ -121,14 +133,25 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
     h.refr_ray_ok = false;
     h.rindex_out = rindex_in;
     cnt.traced++;
+    // :39-49 nearest hit: min distance below 1e6, lowest index on ties.
     float dist = 1000000.0f;
-    int prim = 0, result = 0, hit_once = 0;
-    const int n = S.n;
-    for (int s = 0; s < n; s++) {                       // :39-49 nearest, lowest index on ties
-        int res = intersect(S.type[s], S.geo[s], ray, dist);
-        if (res) { hit_once = 1; prim = s; result = res; }
+    int prim = 0x7fffffff, result = 0;
+#pragma unroll 4
+    for (int k = 0; k < S.ns; k++) {
+        int res;
+        const float c = sphere_cand(S.sph[k], ray, res);
+        const int id = S.sph_id[k];
+        if (res && (c < dist || (c == dist && id < prim))) { dist = c; prim = id; result = res; }
     }
-    cnt.tests += (unsigned long long)n;
+#pragma unroll 4
+    for (int k = 0; k < S.np; k++) {
+        const float c = plane_cand(S.pln[k], ray);
+        const int id = S.pln_id[k];
+        if (c < dist || (c == dist && id < prim)) { dist = c; prim = id; result = 1; }
+    }
+    const int hit_once = prim != 0x7fffffff;
+    if (!hit_once) prim = 0;
+    cnt.tests += (unsigned long long)S.n;
     h.dist = dist;
     if (!hit_once) return h;                            // :51
     h.prim = prim;
@@ -159,13 +182,23 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
             r.o = mk(pi.x + L.x * EPS, pi.y + L.y * EPS, pi.z + L.z * EPS);
             r.d = L;
             cnt.shadow++;
-            int k = 0;
-            const int nn = S.nnonlight;
-            for (; k < nn; k++) {                       // first occluder ends the loop
-                const int s = S.nonlight[k];
-                if (intersect(S.type[s], S.geo[s], r, tdist)) { shade = 0; break; }
+            // Any non-light primitive nearer than the light centre shades the
+            // point (the reference breaks at the first one; which one does not
+            // matter, only the count of tests, recovered from its position).
+            int first = 0x7fffffff;
+#pragma unroll 4
+            for (int k = 0; k < S.nos; k++) {
+                int res;
+                const float c = sphere_cand(S.osph[k], r, res);
+                if (res && c < tdist) first = min(first, S.osph_pos[k]);
             }
-            cnt.tests += (unsigned long long)(k < nn ? k + 1 : nn);
+#pragma unroll 4
+            for (int k = 0; k < S.nop; k++) {
+                const float c = plane_cand(S.opln[k], r);
+                if (c < tdist) first = min(first, S.opln_pos[k]);
+            }
+            if (first != 0x7fffffff) shade = 0;
+            cnt.tests += (unsigned long long)(first != 0x7fffffff ? first + 1 : S.nnonlight);
         }
         if (shade > 0) {                                // :112-174
             v3 L = mk(lg.x, lg.y, lg.z);
@@ -275,12 +308,24 @@ render_kernel(const rt_primitive *__restrict__ prims, int nprims, uint32_t *__re
         S.light[p] = q.m_Light;
     }
     if (threadIdx.x == 0) {
-        int nl = 0, nn = 0;
+        int nl = 0, nn = 0, ns = 0, np = 0, nos = 0, nop = 0;
         for (int p = 0; p < nprims; p++) {
-            if (prims[p].m_Light > 0) S.lights[nl++] = p;
-            if (prims[p].m_Light == 0) S.nonlight[nn++] = p;
+            const rt_primitive &q = prims[p];
+            const bool occluder = q.m_Light == 0;
+            if (q.m_Light > 0) S.lights[nl++] = p;
+            if (q.type == SPHERE) {
+                S.sph[ns] = make_float4(q.m_Centre.x, q.m_Centre.y, q.m_Centre.z, q.m_SqRadius);
+                S.sph_id[ns++] = p;
+                if (occluder) { S.osph[nos] = S.sph[ns - 1]; S.osph_pos[nos++] = nn; }
+            } else if (q.type == PLANE) {
+                S.pln[np] = make_float4(q.plane_N.x, q.plane_N.y, q.plane_N.z, q.plane_D);
+                S.pln_id[np++] = p;
+                if (occluder) { S.opln[nop] = S.pln[np - 1]; S.opln_pos[nop++] = nn; }
+            }
+            if (occluder) nn++;
         }
         S.n = nprims; S.nlights = nl; S.nnonlight = nn;
+        S.ns = ns; S.np = np; S.nos = nos; S.nop = nop;
     }
     __syncthreads();
 
