@@ -71,15 +71,8 @@ __device__ __forceinline__ float sphere_hit(float4 g, const ray3 &r)
     return t1 > EPS ? t1 : (t2 > EPS ? t2 : 0.f);
 }
 
-// Sphere geometry sources for the nearest-hit / any-hit loops.
-//   FixGeo<N>: compile-time sphere count, passed by value as a kernel argument
-//              -> lives in SGPRs, loops fully unrolled (Cornell: N = 9);
-//   DynGeo   : runtime count, LDS (or global) float4 array.
-template <int N> struct FixGeo {
-    float4 g[N];
-    __device__ __forceinline__ constexpr int count() const { return N; }
-    __device__ __forceinline__ float4 at(int i) const { return g[i]; }
-};
+// Sphere geometry for the nearest-hit / any-hit loops: LDS (per-block copy)
+// or global-memory float4 array (scenes above MAXS_LDS), runtime count.
 struct DynGeo {
     const float4 *g;
     int n;
@@ -189,10 +182,9 @@ __device__ __forceinline__ int to_int(float x)
 #ifndef RT_SPT_MINWAVES
 #define RT_SPT_MINWAVES 1   // __launch_bounds__ min waves per SIMD (occupancy A/B builds)
 #endif
-template <int FIXN, bool DL, bool COUNT, bool LDS>
+template <bool DL, bool COUNT, bool LDS>
 __global__ void __launch_bounds__(256, RT_SPT_MINWAVES)
-render_kernel(FixGeo<(FIXN > 0 ? FIXN : 1)> fgeo, const rt_sphere *__restrict__ spheres, int nspheres,
-              rt_camera cam,
+render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,
               uint32_t *seeds_out, uint32_t *__restrict__ pixels, int w, int h,
               int row_begin, int row_end, int first_sample, int nsamples,
@@ -229,12 +221,7 @@ render_kernel(FixGeo<(FIXN > 0 ? FIXN : 1)> fgeo, const rt_sphere *__restrict__ 
         S.geo = g_geo; S.emi = g_emi; S.col = g_col; S.lights = g_lights; S.nlights = g_nlights;
     }
     S.n = nspheres;
-    // Nearest-hit / any-hit geometry: SGPR-resident kernel argument when the
-    // scene size was specialised at compile time, else the LDS/global array.
-    const auto geo = [&]() {
-        if constexpr (FIXN > 0) return fgeo;
-        else return DynGeo{S.geo, S.n};
-    }();
+    const DynGeo geo{S.geo, S.n};
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
@@ -250,31 +237,32 @@ render_kernel(FixGeo<(FIXN > 0 ? FIXN : 1)> fgeo, const rt_sphere *__restrict__ 
             col = mk(colors[3 * (size_t)i], colors[3 * (size_t)i + 1], colors[3 * (size_t)i + 2]);
         const float invW = 1.f / w, invH = 1.f / h;             // :80-81
 
-        int k = 0;
-        bool fresh = true;
         ray3 ray;
-        v3 rad = mk(0.f, 0.f, 0.f), thr = mk(1.f, 1.f, 1.f);
-        int depth = 0;
-        bool specular = true;
+        v3 rad, thr;
+        int depth;
+        bool specular;
+        // :89-105 camera ray; called by the lane that starts a sample, right
+        // after finishing the previous one (one branch for both).
+        const auto camera_ray = [&]() {
+            const float r1 = get_random(s0, s1) - .5f;
+            const float r2 = get_random(s0, s1) - .5f;
+            const float kcx = (x + r1) * invW - .5f;
+            const float kcy = (y + r2) * invH - .5f;
+            v3 rdir = mk(cam.x.x * kcx + cam.y.x * kcy + cam.dir.x,
+                         cam.x.y * kcx + cam.y.y * kcy + cam.dir.y,
+                         cam.x.z * kcx + cam.y.z * kcy + cam.dir.z);
+            v3 rorig = vsmul(0.1f, rdir);
+            rorig = vadd(rorig, mk(cam.orig.x, cam.orig.y, cam.orig.z));
+            rdir = vnorm(rdir);
+            ray.o = rorig; ray.d = rdir;
+            rad = mk(0.f, 0.f, 0.f);
+            thr = mk(1.f, 1.f, 1.f);
+            depth = 0;
+            specular = true;
+        };
+        int k = 0;
+        if (nsamples > 0) camera_ray();
         while (k < nsamples) {
-            if (fresh) {                                        // :89-105 camera ray
-                const float r1 = get_random(s0, s1) - .5f;
-                const float r2 = get_random(s0, s1) - .5f;
-                const float kcx = (x + r1) * invW - .5f;
-                const float kcy = (y + r2) * invH - .5f;
-                v3 rdir = mk(cam.x.x * kcx + cam.y.x * kcy + cam.dir.x,
-                             cam.x.y * kcx + cam.y.y * kcy + cam.dir.y,
-                             cam.x.z * kcx + cam.y.z * kcy + cam.dir.z);
-                v3 rorig = vsmul(0.1f, rdir);
-                rorig = vadd(rorig, mk(cam.orig.x, cam.orig.y, cam.orig.z));
-                rdir = vnorm(rdir);
-                ray.o = rorig; ray.d = rdir;
-                rad = mk(0.f, 0.f, 0.f);
-                thr = mk(1.f, 1.f, 1.f);
-                depth = 0;
-                specular = true;
-                fresh = false;
-            }
             // One bounce of geomfunc.h:182-337.
             bool done = depth > 6;
             if (!done) {
@@ -389,7 +377,7 @@ render_kernel(FixGeo<(FIXN > 0 ? FIXN : 1)> fgeo, const rt_sphere *__restrict__ 
                 }
                 cnt.samples++;
                 k++;
-                fresh = true;
+                if (k < nsamples) camera_ray();
             }
         }
         if (nsamples > 0) {
@@ -418,8 +406,7 @@ render_kernel(FixGeo<(FIXN > 0 ? FIXN : 1)> fgeo, const rt_sphere *__restrict__ 
 #include "rt_runtime.h"
 
 // A prepared scene (spt_scene_create): device AoS copy for the per-block LDS
-// staging, device SoA + light list for scenes above the LDS budget, and the
-// kernel-argument geometry for compile-time-specialised sizes.
+// staging, device SoA + light list for scenes above the LDS budget.
 struct spt_scene {
     int device = -1;
     int n = 0;
@@ -431,21 +418,11 @@ struct spt_scene {
 
 namespace {
 
-constexpr int FIXN_CORNELL = 9;   // CornellSpheres (scene.h:29-40)
-
-template <int FIXN, bool DL, bool COUNT, bool LDS>
+template <bool DL, bool COUNT, bool LDS>
 void launch(dim3 grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam, float *colors,
             const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h, int r0, int r1,
             int first, int ns, unsigned long long *cnt)
 {
-    constexpr int FN = FIXN > 0 ? FIXN : 1;
-    rt::smallpt::FixGeo<FN> fg;
-    for (int i = 0; i < FN; i++) fg.g[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (FIXN > 0)   // centre, rad*rad: the float product SphereIntersect forms (geomfunc.h:42)
-        for (int i = 0; i < FIXN; i++) {
-            const rt_sphere &q = sc.host[i];
-            fg.g[i] = make_float4(q.p.x, q.p.y, q.p.z, q.rad * q.rad);
-        }
     const int n = sc.n;
     const float4 *gg = nullptr, *ge = nullptr, *gc = nullptr;
     const int *gl = nullptr;
@@ -454,22 +431,22 @@ void launch(dim3 grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam,
         gl = (const int *)(gc + n);
     }
     const size_t lds = LDS ? (size_t)n * 3 * sizeof(float4) + (size_t)(n + 1) * sizeof(int) : 0;
-    hipLaunchKernelGGL((rt::smallpt::render_kernel<FIXN, DL, COUNT, LDS>), grid, dim3(256), lds, s, fg,
+    hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, LDS>), grid, dim3(256), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, gg, ge,
                        gc, gl, sc.nlights, cnt);
 }
 
-template <int FIXN, bool LDS>
+template <bool LDS>
 void launch_mode(bool dl, bool count, dim3 grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam,
                  float *colors, const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h,
                  int r0, int r1, int first, int ns, unsigned long long *cnt)
 {
     if (dl) {
-        if (count) launch<FIXN, true, true, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
-        else launch<FIXN, true, false, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+        if (count) launch<true, true, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+        else launch<true, false, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
     } else {
-        if (count) launch<FIXN, false, true, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
-        else launch<FIXN, false, false, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+        if (count) launch<false, true, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+        else launch<false, false, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
     }
 }
 
@@ -553,16 +530,11 @@ extern "C" int spt_scene_render_async(const spt_scene *sc, const rt_camera *came
     hipStream_t s = (hipStream_t)stream;
     unsigned long long *cnt = (unsigned long long *)d_counters;
     const bool dl = mode == SPT_DIRECT_LIGHTING;
-    static const bool no_fix = getenv("RT_SPT_NOFIX") != nullptr;   // A/B switch (tools/ab_smallpt.py)
-    if (sc->n == FIXN_CORNELL && !no_fix)
-        launch_mode<FIXN_CORNELL, true>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in,
-                                        d_seeds_out, d_pixels, w, h, row_begin, row_end, first_sample,
-                                        nsamples, cnt);
-    else if (sc->n <= rt::smallpt::MAXS_LDS)
-        launch_mode<0, true>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
+    if (sc->n <= rt::smallpt::MAXS_LDS)
+        launch_mode<true>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
                              d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
     else
-        launch_mode<0, false>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
+        launch_mode<false>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
                               d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
     return rtrt::check_launch("spt render_kernel");
 }

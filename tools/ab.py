@@ -1,0 +1,82 @@
+"""A/B kernel timing of librt_hip.so builds under build_ab/<name>/ (one child
+process per variant, interleaved rounds, HIP-event time on the launch stream).
+
+    KERNEL=smallpt|whitted LIBS=a,b ROUNDS=2 REPS=5 python tools/ab.py
+
+smallpt: Cornell 1920x1080, SPP (default 64) samples per launch.
+whitted: raytracer3.0.06 scene, 1920x1080, rows [20, H-70).
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "se-195-project-ray-tracer_amd"))
+
+
+def child():
+    import numpy as np
+    import torch
+    import rtamd
+    W, H = 1920, 1080
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    L = rtamd.lib()
+    if os.environ.get("KERNEL", "smallpt") == "whitted":
+        prims, n = rtamd.scenes.whitted_scene()
+        nbytes = C.sizeof(prims)
+        d_prims = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        d_prims.copy_(torch.frombuffer(bytearray(prims), dtype=torch.uint8))
+        px = torch.zeros(W * H, dtype=torch.int32, device=dev)
+
+        def run():
+            rtamd.check(L.rtw_render_async(d_prims.data_ptr(), n, px.data_ptr(), W, H, 20, H - 70, None,
+                                           st.cuda_stream))
+    else:
+        SPP = int(os.environ.get("SPP", "64"))
+        S, n = rtamd.scenes.cornell()
+        cam = rtamd.scenes.cornell_camera(W, H)
+        sc = rtamd.SmallptScene(S, n)
+        seeds0 = torch.from_numpy(rtamd.scenes.seeds(W, H).view(np.int32)).to(dev)
+        seeds = torch.empty_like(seeds0)
+        col = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
+        px = torch.zeros(W * H, dtype=torch.int32, device=dev)
+
+        def run():
+            rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                                 seeds.data_ptr(), px.data_ptr(), W, H, 0, H, 0, SPP, 0,
+                                                 None, st.cuda_stream))
+    run()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(int(os.environ.get("REPS", "5"))):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        run()
+        b.record(st)
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    print("%s %s min %.3f med %.3f ms" % (os.environ.get("KERNEL", "smallpt"), os.environ.get("VARIANT", "?"),
+                                         min(ts), float(np.median(ts))), flush=True)
+
+
+def main():
+    base = os.path.join(ROOT, "build_ab")
+    libs = sorted(os.listdir(base)) if os.path.isdir(base) else []
+    if os.environ.get("LIBS"):
+        libs = os.environ["LIBS"].split(",")
+    variants = {name: {"RT_HIP_LIB": os.path.join(base, name, "librt_hip.so")} for name in libs}
+    if not variants:
+        variants = {"tree": {}}
+    for _ in range(int(os.environ.get("ROUNDS", "2"))):
+        for name, env in variants.items():
+            e = dict(os.environ, VARIANT=name, **env)
+            subprocess.run([sys.executable, __file__, "child"], env=e, check=True, timeout=300)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "child":
+        child()
+    else:
+        main()
