@@ -88,89 +88,28 @@ struct Scene {                // per-block LDS copy (or global view for big scen
     int n, nlights;
 };
 
-// Intersect, geomfunc.h:71-92: i descending, update iff d != 0 && d < t.
-template <class G>
-__device__ __forceinline__ bool intersect(const G &geo, const ray3 &r, float &t, int &id)
+// One ray query over the spheres, i descending, update iff d != 0 && d < t.
+// With t = 1e20f on entry this is Intersect (geomfunc.h:71-92: nearest hit,
+// highest index wins ties); with t = maxt on entry "some update happened" is
+// IntersectP (:94-110: any d != 0 && d < maxt), and the first update is at
+// the index where IntersectP's early exit stops (kept for the test counter).
+// Returns the last updated index, -1 if none.
+template <bool COUNT, class G>
+__device__ __forceinline__ int query(const G &geo, const ray3 &r, float &t, int &first)
 {
-    const float inf = 1e20f;
-    t = inf;
-    id = 0;
+    int id = -1;
 #pragma unroll
     for (int i = geo.count() - 1; i >= 0; i--) {
         const float d = sphere_hit(geo.at(i), r);
         const bool take = (d != 0.f) && (d < t);
         t = take ? d : t;
         id = take ? i : id;
+        if (COUNT) first = (first < 0 && take) ? i : first;
     }
-    return t < inf;
-}
-
-// IntersectP, geomfunc.h:94-110.  All spheres are tested (no divergent early
-// exit); the result and the reference's test count (spheres tested down to and
-// including the first hit in descending order) are recovered from the highest
-// qualifying index.
-template <class G>
-__device__ __forceinline__ bool intersect_p(const G &geo, const ray3 &r, float maxt, unsigned &ntests)
-{
-    int first = -1;
-#pragma unroll
-    for (int i = geo.count() - 1; i >= 0; i--) {
-        const float d = sphere_hit(geo.at(i), r);
-        first = (first < 0 && (d != 0.f) && (d < maxt)) ? i : first;
-    }
-    ntests += first >= 0 ? (unsigned)(geo.count() - first) : (unsigned)geo.count();
-    return first >= 0;
+    return id;
 }
 
 struct Counts { unsigned long long isect, isectp, tests, samples; };
-
-// SampleLights, geomfunc.h:112-165.  UniformSampleSphere's two GetRandom()
-// arguments are drawn second-first, as the g++-built oracle does (:138).
-template <class G>
-__device__ __forceinline__ v3 sample_lights(const G &geo, const Scene &S, uint32_t &s0, uint32_t &s1,
-                                            v3 hit, v3 nl, Counts &cnt)
-{
-    v3 result = mk(0.f, 0.f, 0.f);
-    for (int li = 0; li < S.nlights; li++) {
-        const int i = S.lights[li];
-        const float4 lc = S.col[i];          // colour.xyz, rad
-        const float4 lg = S.geo[i];          // centre
-        const float4 le = S.emi[i];
-        const float rad = lc.w;
-        const float u2 = get_random(s0, s1);
-        const float u1 = get_random(s0, s1);
-        // UniformSampleSphere, geomfunc.h:61-69
-        const float zz = 1.f - 2.f * u1;
-        const float q = 1.f - zz * zz;
-        const float rr = sqrt_rn((0.f > q) ? 0.f : q);
-        const float phi = 2.f * PI_F * u2;
-        float sp_sin, sp_cos;
-        rtm::sincosf(phi, sp_sin, sp_cos);
-        const v3 unit = mk(rr * sp_cos, rr * sp_sin, zz);
-        v3 sp = vsmul(rad, unit);
-        sp = vadd(sp, mk(lg.x, lg.y, lg.z));
-        ray3 sh;
-        sh.o = hit;
-        sh.d = vsub(sp, hit);
-        const float len = sqrt_rn(vdot(sh.d, sh.d));
-        sh.d = vsmul(1.f / len, sh.d);
-        float wo = vdot(sh.d, unit);
-        if (wo > 0.f) continue;
-        wo = -wo;
-        const float wi = vdot(sh.d, nl);
-        if (wi > 0.f) {
-            unsigned nt = 0;
-            cnt.isectp++;
-            const bool occluded = intersect_p(geo, sh, len - EPS, nt);
-            cnt.tests += nt;
-            if (!occluded) {
-                const float s = (4.f * PI_F * rad * rad) * wi * wo / (len * len);
-                result = vadd(result, vsmul(s, mk(le.x, le.y, le.z)));
-            }
-        }
-    }
-    return result;
-}
 
 // toInt, vec.h:62 (clamp macro keeps -0.0; glibc powf via rt_glibc_math.h).
 __device__ __forceinline__ int to_int(float x)
@@ -237,12 +176,25 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             col = mk(colors[3 * (size_t)i], colors[3 * (size_t)i + 1], colors[3 * (size_t)i + 2]);
         const float invW = 1.f / w, invH = 1.f / h;             // :80-81
 
-        ray3 ray;
+        // Per-lane path state.  Every loop iteration issues exactly ONE ray
+        // query for every live lane -- the path ray (nearest hit) or, while a
+        // DIFF vertex is sampling its lights, that light's shadow ray (any hit)
+        // -- so the sphere loop, which is most of the work, runs with all lanes
+        // of the wave active instead of the shadow tests running as a second
+        // loop under the DIFF branch.  Per lane the operations and RNG draws
+        // are the reference's, in its order.
+        ray3 ray;              // the ray queried next
         v3 rad, thr;
         int depth;
         bool specular;
-        // :89-105 camera ray; called by the lane that starts a sample, right
-        // after finishing the previous one (one branch for both).
+        bool shadow = false;   // ray is the shadow ray of light S.lights[li]
+        v3 hit, nl;            // the DIFF vertex (SampleLights' hitPoint, normal)
+        v3 lsum;               // SampleLights' running result
+        float lmax = 0.f;      // shadow ray maxt (len - EPSILON)
+        float lw = 0.f;        // that light's weight s (geomfunc.h:159)
+        int li = 0;
+        // :89-105 camera ray; run by the lane that starts a sample, right after
+        // finishing the previous one (one branch for both).
         const auto camera_ray = [&]() {
             const float r1 = get_random(s0, s1) - .5f;
             const float r2 = get_random(s0, s1) - .5f;
@@ -263,24 +215,33 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         int k = 0;
         if (nsamples > 0) camera_ray();
         while (k < nsamples) {
-            // One bounce of geomfunc.h:182-337.
-            bool done = depth > 6;
-            if (!done) {
-                float t;
-                int id;
+            float t = shadow ? lmax : 1e20f;
+            int first = -1;
+            const int id = query<COUNT>(geo, ray, t, first);
+            bool done = false, lights = false;
+            if (shadow) {                                       // :154-161
+                cnt.isectp++;
+                cnt.tests += first >= 0 ? (unsigned)(S.n - first) : (unsigned)S.n;
+                if (id < 0) {
+                    const float4 le = S.emi[S.lights[li]];
+                    lsum = vadd(lsum, vsmul(lw, mk(le.x, le.y, le.z)));
+                }
+                li++;
+                lights = true;
+            } else {                                            // one bounce of :182-337
                 cnt.isect++;
                 cnt.tests += S.n;
-                if (!intersect(geo, ray, t, id)) {
+                if (id < 0) {
                     done = true;
                 } else {
                     const float4 og = S.geo[id], oe = S.emi[id], oc = S.col[id];
-                    v3 hit = vsmul(t, ray.d);
+                    hit = vsmul(t, ray.d);
                     hit = vadd(ray.o, hit);
                     v3 normal = vsub(hit, mk(og.x, og.y, og.z));
                     normal = vnorm(normal);
                     const float dp = vdot(normal, ray.d);
                     const float inv_sign = -1.f * (dp > 0 ? 1.f : -1.f);
-                    const v3 nl = vsmul(inv_sign, normal);
+                    nl = vsmul(inv_sign, normal);
                     const int refl = __float_as_int(oe.w);
                     if (!((oe.x == 0.f) && (oe.x == 0.f) && (oe.z == 0.f))) {
                         if (specular) {
@@ -292,28 +253,9 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     } else if (refl == DIFF) {
                         specular = false;
                         thr = vmul(thr, mk(oc.x, oc.y, oc.z));
-                        v3 ld = sample_lights(geo, S, s0, s1, hit, nl, cnt);
-                        ld = vmul(thr, ld);
-                        rad = vadd(rad, ld);
-                        if (DL) {
-                            done = true;
-                        } else {
-                            const float r1 = 2.f * PI_F * get_random(s0, s1);
-                            const float r2 = get_random(s0, s1);
-                            const float r2s = sqrt_rn(r2);
-                            const v3 wv = nl;
-                            const v3 a = (fabsf(wv.x) > .1f) ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
-                            v3 u = vnorm(vxcross(a, wv));
-                            v3 v = vxcross(wv, u);
-                            float sn1, cs1;
-                            rtm::sincosf(r1, sn1, cs1);
-                            u = vsmul(cs1 * r2s, u);
-                            v = vsmul(sn1 * r2s, v);
-                            v3 nd = vadd(u, v);
-                            nd = vadd(nd, vsmul(sqrt_rn(1 - r2), wv));
-                            ray.o = hit;
-                            ray.d = nd;
-                        }
+                        lsum = mk(0.f, 0.f, 0.f);
+                        li = 0;
+                        lights = true;
                     } else if (refl == SPEC) {
                         specular = true;
                         v3 nd = vsmul(2.f * vdot(normal, ray.d), normal);
@@ -362,6 +304,69 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                         }
                     }
                     depth++;
+                    done = done || (!lights && depth > 6);      // :184 at the next bounce
+                }
+            }
+            if (lights) {
+                // SampleLights (:112-165) from light li on: stop at the next
+                // light that needs a shadow test; UniformSampleSphere's two
+                // GetRandom() arguments are drawn second-first, as the g++-built
+                // oracle does (:138).
+                shadow = false;
+                for (; li < S.nlights; li++) {
+                    const int i = S.lights[li];
+                    const float4 lc = S.col[i];                 // colour.xyz, rad
+                    const float4 lg = S.geo[i];                 // centre
+                    const float lrad = lc.w;
+                    const float u2 = get_random(s0, s1);
+                    const float u1 = get_random(s0, s1);
+                    const float zz = 1.f - 2.f * u1;            // UniformSampleSphere, :61-69
+                    const float q = 1.f - zz * zz;
+                    const float rr = sqrt_rn((0.f > q) ? 0.f : q);
+                    const float phi = 2.f * PI_F * u2;
+                    float sp_sin, sp_cos;
+                    rtm::sincosf(phi, sp_sin, sp_cos);
+                    const v3 unit = mk(rr * sp_cos, rr * sp_sin, zz);
+                    v3 sp = vsmul(lrad, unit);
+                    sp = vadd(sp, mk(lg.x, lg.y, lg.z));
+                    v3 sd = vsub(sp, hit);
+                    const float len = sqrt_rn(vdot(sd, sd));
+                    sd = vsmul(1.f / len, sd);
+                    float wo = vdot(sd, unit);
+                    if (wo > 0.f) continue;
+                    wo = -wo;
+                    const float wi = vdot(sd, nl);
+                    if (wi > 0.f) {
+                        ray.o = hit;
+                        ray.d = sd;
+                        lmax = len - EPS;
+                        lw = (4.f * PI_F * lrad * lrad) * wi * wo / (len * len);
+                        shadow = true;
+                        break;
+                    }
+                }
+                if (!shadow) {                                  // :229-269
+                    rad = vadd(rad, vmul(thr, lsum));
+                    if (DL) {
+                        done = true;
+                    } else {
+                        const float r1 = 2.f * PI_F * get_random(s0, s1);
+                        const float r2 = get_random(s0, s1);
+                        const float r2s = sqrt_rn(r2);
+                        const v3 wv = nl;
+                        const v3 a = (fabsf(wv.x) > .1f) ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
+                        v3 u = vnorm(vxcross(a, wv));
+                        v3 v = vxcross(wv, u);
+                        float sn1, cs1;
+                        rtm::sincosf(r1, sn1, cs1);
+                        u = vsmul(cs1 * r2s, u);
+                        v = vsmul(sn1 * r2s, v);
+                        v3 nd = vadd(u, v);
+                        nd = vadd(nd, vsmul(sqrt_rn(1 - r2), wv));
+                        ray.o = hit;
+                        ray.d = nd;
+                        done = depth > 6;
+                    }
                 }
             }
             if (done) {                                         // :110-118 running average
