@@ -40,6 +40,54 @@ __device__ __forceinline__ float sqrt_rn(float x)
     return tiny ? s * 0x1p-16f : s;
 }
 
+// Short correctly rounded forms on the normal range, each checked against the
+// IEEE result for all 2^32 inputs on the device (tests/test_gpu_math.py):
+//  * sqrt_nr: v_sqrt_f32, then one residual correction s + (x - s*s) / (2s)
+//    with 1/(2s) from v_rsq_f32 -- equal to sqrtf(x) for x in [2^-96, inf)
+//    (differences start below 2^-102);
+//  * rcp_nr: v_rcp_f32 and one Newton step -- equal to 1.f / x for
+//    2^-126 <= |x| < 2^126 (outside it the result or input is denormal).
+// Callers guard the domain with a wave-uniform branch to the general
+// sequences (sqrt_rn, '/'), so a wave only pays for those when one of its
+// lanes is outside the range.
+__device__ __forceinline__ bool sqrt_nr_ok(float x)     // 2^-96 <= x < +inf (not NaN)
+{
+    return (__float_as_uint(x) - 0x0f800000u) < 0x70000000u;
+}
+
+__device__ __forceinline__ float sqrt_nr(float x)
+{
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float h = 0.5f * __builtin_amdgcn_rsqf(x);
+    const float r = __builtin_fmaf(-s, s, x);
+    return __builtin_fmaf(r, h, s);
+}
+
+__device__ __forceinline__ float rcp_nr(float x)
+{
+    const float y = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, y, 1.f);
+    return __builtin_fmaf(e, y, y);
+}
+
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
+// sqrtf(x), bit-exact for every x.
+__device__ __forceinline__ float sqrt_exact(float x)
+{
+    if (!wave_any(!sqrt_nr_ok(x))) return sqrt_nr(x);
+    return sqrt_rn(x);
+}
+
+// 1.f / sqrtf(d), bit-exact for every d (the reference's normalisation factor:
+// vec.h:50 vnorm, common.h:19 NORMALIZE).  For d in sqrt_nr's range sqrtf(d)
+// lies in [2^-48, 2^64), inside rcp_nr's range.
+__device__ __forceinline__ float inv_len(float d)
+{
+    if (!wave_any(!sqrt_nr_ok(d))) return rcp_nr(sqrt_nr(d));
+    return 1.f / sqrt_rn(d);
+}
+
 // Wave-level u64 sum (64 lanes) used for the optional work counters.
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 {

@@ -50,7 +50,7 @@ __device__ __forceinline__ v3 vsmul(float k, v3 b) { return mk(k * b.x, k * b.y,
 __device__ __forceinline__ v3 vadd(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ v3 vsub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ v3 vmul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ v3 vnorm(v3 v) { const float l = 1.f / sqrt_rn(vdot(v, v)); return vsmul(l, v); }
+__device__ __forceinline__ v3 vnorm(v3 v) { const float l = inv_len(vdot(v, v)); return vsmul(l, v); }
 __device__ __forceinline__ v3 vxcross(v3 a, v3 b)
 {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -66,7 +66,7 @@ __device__ __forceinline__ float sphere_hit(float4 g, const ray3 &r)
     const float b = opx * r.d.x + opy * r.d.y + opz * r.d.z;
     const float det = b * b - (opx * opx + opy * opy + opz * opz) + g.w;
     if (det < 0.f) return 0.f;
-    const float sd = sqrt_rn(det);
+    const float sd = sqrt_exact(det);
     const float t1 = b - sd, t2 = b + sd;
     return t1 > EPS ? t1 : (t2 > EPS ? t2 : 0.f);
 }
@@ -98,7 +98,7 @@ template <bool COUNT, class G>
 __device__ __forceinline__ int query(const G &geo, const ray3 &r, float &t, int &first)
 {
     int id = -1;
-#pragma unroll
+#pragma unroll 1
     for (int i = geo.count() - 1; i >= 0; i--) {
         const float d = sphere_hit(geo.at(i), r);
         const bool take = (d != 0.f) && (d < t);
@@ -277,7 +277,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                             ray.o = hit;
                             ray.d = nd;
                         } else {
-                            const float kk = (into ? 1.f : -1.f) * (ddn * nnt + sqrt_rn(cos2t));
+                            const float kk = (into ? 1.f : -1.f) * (ddn * nnt + sqrt_exact(cos2t));
                             const v3 nkk = vsmul(kk, normal);
                             v3 td = vsmul(nnt, ray.d);
                             td = vsub(td, nkk);
@@ -322,7 +322,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     const float u1 = get_random(s0, s1);
                     const float zz = 1.f - 2.f * u1;            // UniformSampleSphere, :61-69
                     const float q = 1.f - zz * zz;
-                    const float rr = sqrt_rn((0.f > q) ? 0.f : q);
+                    const float rr = sqrt_exact((0.f > q) ? 0.f : q);
                     const float phi = 2.f * PI_F * u2;
                     float sp_sin, sp_cos;
                     rtm::sincosf(phi, sp_sin, sp_cos);
@@ -330,8 +330,16 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     v3 sp = vsmul(lrad, unit);
                     sp = vadd(sp, mk(lg.x, lg.y, lg.z));
                     v3 sd = vsub(sp, hit);
-                    const float len = sqrt_rn(vdot(sd, sd));
-                    sd = vsmul(1.f / len, sd);
+                    const float dd = vdot(sd, sd);
+                    float len, ilen;
+                    if (!wave_any(!sqrt_nr_ok(dd))) {
+                        len = sqrt_nr(dd);
+                        ilen = rcp_nr(len);
+                    } else {
+                        len = sqrt_rn(dd);
+                        ilen = 1.f / len;
+                    }
+                    sd = vsmul(ilen, sd);
                     float wo = vdot(sd, unit);
                     if (wo > 0.f) continue;
                     wo = -wo;
@@ -352,7 +360,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     } else {
                         const float r1 = 2.f * PI_F * get_random(s0, s1);
                         const float r2 = get_random(s0, s1);
-                        const float r2s = sqrt_rn(r2);
+                        const float r2s = sqrt_exact(r2);
                         const v3 wv = nl;
                         const v3 a = (fabsf(wv.x) > .1f) ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
                         v3 u = vnorm(vxcross(a, wv));
@@ -362,7 +370,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                         u = vsmul(cs1 * r2s, u);
                         v = vsmul(sn1 * r2s, v);
                         v3 nd = vadd(u, v);
-                        nd = vadd(nd, vsmul(sqrt_rn(1 - r2), wv));
+                        nd = vadd(nd, vsmul(sqrt_exact(1 - r2), wv));
                         ray.o = hit;
                         ray.d = nd;
                         done = depth > 6;
@@ -375,7 +383,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     col = rad;
                 } else {
                     const float k1 = (float)current;
-                    const float k2 = 1.f / (k1 + 1.f);
+                    const float k2 = rcp_nr(k1 + 1.f);      // 2 <= k1 + 1 <= 2^31: rcp_nr range
                     col.x = (col.x * k1 + rad.x) * k2;
                     col.y = (col.y * k1 + rad.y) * k2;
                     col.z = (col.z * k1 + rad.z) * k2;

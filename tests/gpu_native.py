@@ -19,6 +19,13 @@ DOMAINS = [
     ("sincosf_cos_neg", 6, 0x80000000, 0xc1000000),
     ("sqrt_rn_pos", 7, 0x00000000, 0x7fffffff),  # rt_common.h sqrt_rn: every non-negative float, NaNs
     ("sqrt_rn_neg", 7, 0x80000000, 0xffffffff),  # every negative float (NaN results, -0)
+    # rt_common.h short forms: sqrt_nr / rcp_nr on their stated ranges, and the
+    # guarded sqrt_exact / inv_len (uniform fallback) on every float
+    ("sqrt_nr_range", 11, 0x0f800000, 0x7f7fffff),   # [2^-96, FLT_MAX]
+    ("rcp_nr_range", 10, 0x00800000, 0x7c7fffff),    # [2^-126, 2^126)
+    ("rcp_nr_range_neg", 10, 0x80800000, 0xfc7fffff),
+    ("sqrt_exact_all", 8, 0x00000000, 0xffffffff),
+    ("inv_len_all", 9, 0x00000000, 0xffffffff),
 ]
 
 

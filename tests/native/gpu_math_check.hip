@@ -26,8 +26,14 @@ __device__ __host__ inline float eval(int fn, float x)
 
 __device__ inline float eval_dev(int fn, float x)
 {
-    if (fn == 7) return rt::sqrt_rn(x);
-    return eval(fn, x);
+    switch (fn) {
+    case 7: return rt::sqrt_rn(x);
+    case 8: return rt::sqrt_exact(x);
+    case 9: return rt::inv_len(x);
+    case 10: return rt::rcp_nr(x);
+    case 11: return rt::sqrt_nr(x);
+    default: return eval(fn, x);
+    }
 }
 
 static float host_glibc(int fn, float x)
@@ -37,7 +43,9 @@ static float host_glibc(int fn, float x)
     case 1: return ::powf(x, 1.f / 2.2f);
     case 2: return ::expf(x);
     case 3: case 5: return ::sinf(x);
-    case 7: return ::sqrtf(x);
+    case 7: case 8: case 11: return ::sqrtf(x);
+    case 9: return 1.f / ::sqrtf(x);
+    case 10: return 1.f / x;
     default: return ::cosf(x);
     }
 }

@@ -57,6 +57,13 @@ def child():
         b.record(st)
         torch.cuda.synchronize()
         ts.append(a.elapsed_time(b))
+    if os.environ.get("PROF"):      # block counters of a tools-only instrumented build
+        buf = (C.c_ulonglong * 18)()
+        L.spt_prof_read(buf)
+        names = ["iter", "shadow", "nearest", "diff", "spec", "refr", "light", "bounce", "done"]
+        for b, nm in enumerate(names):
+            lanes, waves = buf[2 * b], buf[2 * b + 1]
+            print("  %-8s lanes %14d waves %12d lanes/wave-exec %.1f" % (nm, lanes, waves, lanes / max(waves, 1)))
     print("%s %s min %.3f med %.3f ms" % (os.environ.get("KERNEL", "smallpt"), os.environ.get("VARIANT", "?"),
                                          min(ts), float(np.median(ts))), flush=True)
 
