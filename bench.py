@@ -16,6 +16,7 @@ IntersectP calls, counted by the kernel itself.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
+import glob
 import ctypes as C
 import json
 import os
@@ -36,6 +37,23 @@ from rtamd import dist as rdist  # noqa: E402
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: peak FP32 vector
 W, H, SPP = 1920, 1080, 64
+
+
+BENCH_KERNEL = "rt::smallpt::render_kernel<false, false, true>"
+
+
+def pmc_digest(kernel):
+    """Per-launch PMC figures for `kernel` from the newest committed
+    profiles/rNN/pmc_digest.json (written by tools/prof_round.sh +
+    tools/pmc_digest.py from rocprofv3 --pmc passes of this bench command)."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_digest.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if kernel in d:
+            return d[kernel], os.path.relpath(f, ROOT)
+    return None, None
 
 
 def parse():
@@ -200,6 +218,7 @@ def main():
     launch_bytes = 32 * B * W + 44 * ns
     achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
     flops = 20.0 * counts[2] / world
+    pmc, pmc_src = pmc_digest(BENCH_KERNEL) if world == 1 else (None, None)
     out = {
         "metric": "Mrays/sec + ms/frame @1920x1080 Cornell-64spp, 1/2/4/8 GPU; % HBM roofline",
         "value": round(rays_per_frame / (ms_per_step * 1e-3) / 1e6, 2),
@@ -221,13 +240,20 @@ def main():
         "rays_per_frame": rays_per_frame,
         "kernel_ms": round(kern_ms, 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": int(pmc["traffic_bytes"]) if pmc and "traffic_bytes" in pmc else None,
+                     "traffic_source": pmc_src,
+                     "algorithmic_bytes": launch_bytes,
                      "note": "compute-bound kernel: HBM roofline reported because the metric asks; "
                              "see valu"},
         "valu": {"achieved_tflops": round(flops / (kern_ms * 1e-3) / 1e12, 3),
                  "peak_tflops": FP32_PEAK_TFLOPS,
                  "frac": flops / (kern_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
-                 "basis": "20 FLOP per ray-sphere test"},
+                 "basis": "20 FLOP per ray-sphere test",
+                 "issue_frac": round(pmc["valu_issue_frac"], 4) if pmc and "valu_issue_frac" in pmc else None,
+                 "lane_util": round(pmc["lane_util"], 4) if pmc and "lane_util" in pmc else None,
+                 "issue_basis": "SQ_INSTS_VALU x 2 cycles (wave64 on SIMD32) / (1024 SIMDs x 2.4 GHz x "
+                                "kernel time), from the PMC digest"},
     }
     if rank == 0 and world == 1:
         if not args.no_whitted:

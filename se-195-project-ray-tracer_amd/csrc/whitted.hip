@@ -73,7 +73,7 @@ __device__ __forceinline__ float sphere_cand(float4 g, const ray3 &r, int &res)
     res = 0;
     float cand = __builtin_inff();
     if (det > 0) {
-        det = sqrt_rn(det);
+        det = sqrt_exact(det);
         const float i1 = b - det, i2 = b + det;
         if (i2 > 0) {
             cand = i1 < 0 ? i2 : i1;
@@ -175,8 +175,15 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
         float shade = 1.0f;
         if (S.type[l] == SPHERE) {                      // :76-110
             v3 L = mk(lg.x - pi.x, lg.y - pi.y, lg.z - pi.z);
-            float tdist = sqrt_rn(L.x * L.x + L.y * L.y + L.z * L.z);
-            float inv = 1.0f / tdist;
+            const float d2 = L.x * L.x + L.y * L.y + L.z * L.z;
+            float tdist, inv;
+            if (!wave_any(!sqrt_nr_ok(d2))) {
+                tdist = sqrt_nr(d2);
+                inv = rcp_nr(tdist);
+            } else {
+                tdist = sqrt_rn(d2);
+                inv = 1.0f / tdist;
+            }
             L.x *= inv; L.y *= inv; L.z *= inv;
             ray3 r;
             r.o = mk(pi.x + L.x * EPS, pi.y + L.y * EPS, pi.z + L.z * EPS);
@@ -203,9 +210,16 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
         if (shade > 0) {                                // :112-174
             v3 L = mk(lg.x, lg.y, lg.z);
             L.x -= pi.x; L.y -= pi.y; L.z -= pi.z;
-            float len = sqrt_rn(L.x * L.x + L.y * L.y + L.z * L.z);
+            const float d2 = L.x * L.x + L.y * L.y + L.z * L.z;
+            float len, inv;
+            if (!wave_any(!sqrt_nr_ok(d2))) {
+                len = sqrt_nr(d2);
+                inv = rcp_nr(len);
+            } else {
+                len = sqrt_rn(d2);
+                inv = 1.0f / len;
+            }
             if (len > 0.0f) {
-                float inv = 1.0f / len;
                 L.x *= inv; L.y *= inv; L.z *= inv;
             } else {
                 L = mk(0.f, 0.f, 0.f);
@@ -243,7 +257,7 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
         cosI = -cosI;
         float cosT2 = 1.0f - nr * nr * (1.0f - cosI * cosI);
         if (cosT2 > 0.0f) {
-            float k = nr * cosI - sqrt_rn(cosT2);
+            float k = nr * cosI - sqrt_exact(cosT2);
             v3 T = mk((nr * ray.d.x) + k * Nr.x, (nr * ray.d.y) + k * Nr.y, (nr * ray.d.z) + k * Nr.z);
             h.refr_ray.o = mk(pi.x + T.x * EPS, pi.y + T.y * EPS, pi.z + T.z * EPS);
             h.refr_ray.d = T;
@@ -269,7 +283,7 @@ __device__ __forceinline__ ray3 primary(int sub, float SX, float SY, float DX, f
     d.x = (SX + DX * tx / 2.0f) - 0.0f;
     d.y = (SY + DY * ty / 2.0f) - 0.25f;
     d.z = 0.0f - (-7.0f);
-    float l = 1.0f / sqrt_rn(d.x * d.x + d.y * d.y + d.z * d.z);
+    float l = inv_len(d.x * d.x + d.y * d.y + d.z * d.z);
     d.x *= l; d.y *= l; d.z *= l;
     ray3 r;
     r.o = mk(0.0f, 0.25f, -7.0f);
