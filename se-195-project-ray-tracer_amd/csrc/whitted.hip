@@ -7,22 +7,21 @@
 // packed to 0x00RRGGBB with the x28 scale and 255 clamp (:517-523).
 //
 // Mapping (MI355X-first, not a port of openCLcode.cl):
-//   * one lane per pixel; a wave owns an 8x8 pixel tile (coherent trees),
-//     a 256-thread block a 16x16 tile;
+//   * the ray trees of all (pixel, sub-sample) pairs are evaluated level by
+//     level (see "Level-synchronous" below): one coherent launch for the 9 x
+//     W x rows root rays, then one launch per tree level over a compacted
+//     queue of child rays, back-accumulation level by level, and a final
+//     per-pixel sum.  Every lane traces one ray per step (no lane idles while
+//     a neighbour walks a deep glass tree), and the node records live in a
+//     device arena written once and read once (no per-lane scratch arrays);
 //   * the <= 64 primitives are staged once per block from the reference's
 //     96-byte AoS into LDS as SoA (geometry float4, materials, light list);
 //     the nearest-hit and occluder loops read them with wave-uniform indices
 //     (LDS broadcast, no bank conflicts);
-//   * the ray tree runs in the reference's breadth-first order from a 64-bit
-//     "to do" mask (ctz = next node), so the stale-refraction-ray quirk after
-//     total internal reflection (raytracer.cpp:231-233) is reproduced
-//     exactly; the nine sub-samples and their trees form ONE per-lane work
-//     loop (a lane that finishes a small tree starts its next sub-sample
-//     while others still trace), so a wave's cost is the max over lanes of
-//     the whole pixel's traced rays, not of each sub-sample's;
-//   * per-node tree records live in per-lane private memory (touched only for
-//     traced nodes); the running ray, its shading and the occluder loops stay
-//     in VGPRs;
+//   * trees the level pass cannot evaluate exactly -- total internal
+//     reflection, whose refraction child reuses the previous node's
+//     refraction ray (raytracer.cpp:231-233), or a full queue -- are
+//     re-evaluated by a sequential per-lane BFS (fixup_kernel);
 //   * m_SX / m_SY are sequential float sums in the reference (:309,:524,:526):
 //     the host tabulates them once per frame size (exact same float adds);
 //   * glibc powf/expf are reproduced by rt_glibc_math.h (double-precision,
@@ -136,7 +135,6 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
     // :39-49 nearest hit: min distance below 1e6, lowest index on ties.
     float dist = 1000000.0f;
     int prim = 0x7fffffff, result = 0;
-#pragma unroll 4
     for (int k = 0; k < S.ns; k++) {
         int res;
         const float c = sphere_cand(S.sph[k], ray, res);
@@ -193,7 +191,6 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
             // point (the reference breaks at the first one; which one does not
             // matter, only the count of tests, recovered from its position).
             int first = 0x7fffffff;
-#pragma unroll 4
             for (int k = 0; k < S.nos; k++) {
                 int res;
                 const float c = sphere_cand(S.osph[k], r, res);
@@ -291,24 +288,9 @@ __device__ __forceinline__ ray3 primary(int sub, float SX, float SY, float DX, f
     return r;
 }
 
-struct NodeStore {       // per-lane private tree records (only traced nodes touched)
-    float4 col[NODES];   // colour.xyz, dist
-    int info[NODES];     // hit primitive | (TIR << 8)
-    float4 ra[NODES];    // refl ray o.xyz, d.x
-    float4 rb[NODES];    // refl ray d.yz, refr ray o.xy
-    float4 rc[NODES];    // refr ray o.z, d.xyz
-    float rin[NODES];    // *a_RIndex after the node's call
-};
-
-template <bool COUNT>
-__global__ void __launch_bounds__(256)
-render_kernel(const rt_primitive *__restrict__ prims, int nprims, uint32_t *__restrict__ out,
-              int w, int row_begin, int row_end, const float *__restrict__ sx_tab,
-              const float *__restrict__ sy_tab, float DX, float DY,
-              unsigned long long *__restrict__ counters)
+// Stages the reference's 96-byte AoS primitives into the block's LDS SoA.
+__device__ void stage_scene(Scene &S, const rt_primitive *__restrict__ prims, int nprims)
 {
-    __shared__ Scene S;
-    // Stage the reference's 96-byte AoS primitives into LDS SoA.
     for (int p = threadIdx.x; p < nprims; p += blockDim.x) {
         const rt_primitive &q = prims[p];
         const bool sph = q.type == SPHERE;
@@ -342,43 +324,326 @@ render_kernel(const rt_primitive *__restrict__ prims, int nprims, uint32_t *__re
         S.ns = ns; S.np = np; S.nos = nos; S.nop = nop;
     }
     __syncthreads();
+}
 
+// ---------------------------------------------------------------------------
+// Level-synchronous ("wavefront") evaluation of the ray trees.
+//
+// A tree = one (pixel, sub-sample) of Engine_Render; node i of the reference's
+// 63-slot BFS array sits on level floor(log2(i+1)).  The reference traces a
+// child of node p iff p < 31 and refl/refr(p) > 0 (:398-472), with p's own
+// reflection ray and -- unless p had total internal reflection -- p's own
+// refraction ray; the trace of a node depends on nothing else.  So all trees
+// advance together one level per launch:
+//   root_kernel    level 0 of every tree (coherent: one launch, lanes = pixels);
+//   level_kernel   level L = 1..5 from a compacted queue of child rays that
+//                  level L-1 appended (wave-aggregated atomics);
+//   backacc_kernel levels 4..1: node colour += refraction child (Beer factor)
+//                  then += reflection child (:476-511), children final first;
+//   final_kernel   level 0 of the nine trees of a pixel + the sum / x28 pack.
+// Records hold what back-accumulation needs (colour, distance, primitive, TIR)
+// and the queue slots of the node's two children.
+//
+// Exceptions go to fixup_kernel, which re-evaluates the whole tree in the
+// reference's sequential BFS order (per-lane records):
+//   * TIR: the reference still traces p's refraction child, with the
+//     refraction ray of the last node BEFORE p in BFS order that wrote one
+//     (:231-233, a stale variable) -- a cross-node dependency.  The wavefront
+//     does not trace that child and flags the tree;
+//   * a full child queue (capacity = number of trees per level).
+// The fixup counts only the nodes the wavefront did not trace, so counters
+// stay exactly the reference's.
+constexpr int LEVELS = 6;
+constexpr int INFO_TIR = 0x100;
+
+struct WfArgs {
+    float4 *rcol;             // [ntrees] root colour.xyz, dist
+    int *rinfo;               // [ntrees] hit primitive | INFO_TIR
+    int2 *rchild;             // [ntrees] queue slots (level 1) of refl / refr child, -1 if none
+    int *fixflag;             // [ntrees] 0, or -1 once queued for fixup
+    int *fixlist;             // [ntrees] trees to fix
+    float4 *ia[LEVELS];       // [cap] queued ray: o.xyz, d.x
+    float4 *ib[LEVELS];       // [cap] d.y, d.z, rindex, tree (int bits)
+    float4 *lcol[LEVELS];     // [cap] node colour.xyz, dist
+    int *linfo[LEVELS];       // [cap] hit primitive | INFO_TIR
+    int2 *lchild[LEVELS];     // [cap] child slots in level L+1
+    int *count;               // [LEVELS] queue lengths (index 1..5), [LEVELS] fixup count
+    int cap, ntrees, npix, w, row_begin;
+};
+
+__device__ void flag_tree(const WfArgs &A, int tree)
+{
+    if (atomicCAS(&A.fixflag[tree], 0, -1) == 0) {
+        const int s = atomicAdd(&A.count[LEVELS], 1);
+        A.fixlist[s] = tree;
+    }
+}
+
+// Wave-aggregated queue allocation: every active lane asks for `want` (0..2)
+// slots; one atomic per wave.  Returns the lane's first slot.
+__device__ __forceinline__ int wave_alloc(int *counter, int want)
+{
+    const unsigned long long m1 = __builtin_amdgcn_ballot_w64((want & 1) != 0);
+    const unsigned long long m2 = __builtin_amdgcn_ballot_w64((want & 2) != 0);
+    const int lane = __lane_id();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int pre = __popcll(m1 & lt) + 2 * __popcll(m2 & lt);
+    const int tot = __popcll(m1) + 2 * __popcll(m2);
+    const int first = __builtin_ctzll(__builtin_amdgcn_read_exec());
+    int base = 0;
+    if (lane == first && tot) base = atomicAdd(counter, tot);
+    base = __shfl(base, first, 64);
+    return base + pre;
+}
+
+// Queues the children of a just-traced node (level L < 5) into level L+1 and
+// returns their slots (-1: not queued).  All lanes of the wave call it.
+__device__ __forceinline__ int2 queue_children(const WfArgs &A, int L, bool active, int tree, const Hit &hh,
+                                               bool tir)
+{
+    const bool cl = active && hh.refl > 0, cr = active && hh.refr > 0;
+    const bool qr = cr && !tir;
+    int slot = wave_alloc(&A.count[L + 1], (int)cl + (int)qr);
+    int2 ch = make_int2(-1, -1);
+    if (cl) {
+        if (slot < A.cap) {
+            const ray3 &r = hh.refl_ray;
+            A.ia[L + 1][slot] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+            A.ib[L + 1][slot] = make_float4(r.d.y, r.d.z, hh.rindex_out, __int_as_float(tree));
+            ch.x = slot;
+        } else {
+            flag_tree(A, tree);
+        }
+        slot++;
+    }
+    if (cr) {
+        if (tir) {
+            flag_tree(A, tree);
+        } else if (slot < A.cap) {
+            const ray3 &r = hh.refr_ray;
+            A.ia[L + 1][slot] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+            A.ib[L + 1][slot] = make_float4(r.d.y, r.d.z, hh.rindex_out, __int_as_float(tree));
+            ch.y = slot;
+        } else {
+            flag_tree(A, tree);
+        }
+    }
+    return ch;
+}
+
+template <bool COUNT>
+__global__ void __launch_bounds__(256)
+root_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A, int row_end,
+            const float *__restrict__ sx_tab, const float *__restrict__ sy_tab, float DX, float DY,
+            unsigned long long *__restrict__ counters)
+{
+    __shared__ Scene S;
+    stage_scene(S, prims, nprims);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int y = row_begin + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool active = x < w && y < row_end;
-
+    const int y = A.row_begin + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool active = x < A.w && y < row_end;
+    const int pix = (y - A.row_begin) * A.w + x;
+    const float SX = active ? sx_tab[x] : 0.f, SY = active ? sy_tab[y] : 0.f;
     Counts cnt = {0, 0, 0, 0};
-    if (active) {
-        const float SX = sx_tab[x], SY = sy_tab[y];
+    for (int sub = 0; sub < 9; sub++) {
+        Hit hh;
+        bool tir = false;
+        if (active) {
+            hh = trace(S, primary(sub, SX, SY, DX, DY), 1.0f, cnt);
+            tir = hh.refr > 0 && !hh.refr_ray_ok;
+            if (tir) cnt.tir++;
+        }
+        const int tree = sub * A.npix + pix;
+        const int2 ch = queue_children(A, 0, active, tree, hh, tir);
+        if (active) {
+            A.rcol[tree] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
+            A.rinfo[tree] = (hh.prim & 0xff) | (tir ? INFO_TIR : 0);
+            A.rchild[tree] = ch;
+        }
+    }
+    if (COUNT) {
+        const unsigned long long c[4] = {cnt.traced, cnt.shadow, cnt.tests, cnt.tir};
+        flush_counters<4>(counters, c);
+    }
+}
+
+template <bool COUNT>
+__global__ void __launch_bounds__(256)
+level_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A, int L,
+             unsigned long long *__restrict__ counters)
+{
+    __shared__ Scene S;
+    stage_scene(S, prims, nprims);
+    const int n = min(A.count[L], A.cap);
+    Counts cnt = {0, 0, 0, 0};
+    for (int base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {   // block-uniform trip count
+        const int q = base + threadIdx.x;
+        const bool active = q < n;
+        Hit hh;
+        bool tir = false;
+        int tree = 0;
+        if (active) {
+            const float4 a = A.ia[L][q], b = A.ib[L][q];
+            ray3 r;
+            r.o = mk(a.x, a.y, a.z);
+            r.d = mk(a.w, b.x, b.y);
+            tree = __float_as_int(b.w);
+            hh = trace(S, r, b.z, cnt);
+            tir = hh.refr > 0 && !hh.refr_ray_ok;
+            if (tir && L < 5) cnt.tir++;                // node index < 31 (:398)
+            A.lcol[L][q] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
+            A.linfo[L][q] = (hh.prim & 0xff) | (tir ? INFO_TIR : 0);
+        }
+        if (L < 5) {
+            const int2 ch = queue_children(A, L, active, tree, hh, tir);
+            if (active) A.lchild[L][q] = ch;
+        }
+    }
+    if (COUNT) {
+        const unsigned long long c[4] = {cnt.traced, cnt.shadow, cnt.tests, cnt.tir};
+        flush_counters<4>(counters, c);
+    }
+}
+
+// Back-accumulation of one node (raytracer.cpp:476-511): the refraction child
+// (Beer factor from the node's own distance and colour, unless TIR) first,
+// then the reflection child (colour x refl).
+__device__ __forceinline__ float4 accumulate(const Scene &S, float4 pc, int pinfo, int2 ch,
+                                             const float4 *__restrict__ ccol)
+{
+    const float4 pm = S.mat0[pinfo & 0xff];
+    if (ch.y >= 0) {
+        const float4 cc = ccol[ch.y];
+        float ax = cc.x, ay = cc.y, az = cc.z;
+        if (!(pinfo & INFO_TIR)) {
+            const float nd = -pc.w;
+            ax = cc.x * rtm::expf(pm.x * 0.15f * nd);
+            ay = cc.y * rtm::expf(pm.y * 0.15f * nd);
+            az = cc.z * rtm::expf(pm.z * 0.15f * nd);
+        }
+        pc.x += ax; pc.y += ay; pc.z += az;
+    }
+    if (ch.x >= 0) {
+        const float4 cc = ccol[ch.x];
+        pc.x += cc.x * pm.x * pm.w;
+        pc.y += cc.y * pm.y * pm.w;
+        pc.z += cc.z * pm.z * pm.w;
+    }
+    return pc;
+}
+
+__global__ void __launch_bounds__(256)
+backacc_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A, int L)
+{
+    __shared__ Scene S;
+    stage_scene(S, prims, nprims);
+    const int n = min(A.count[L], A.cap);
+    for (int q = blockIdx.x * 256 + threadIdx.x; q < n; q += gridDim.x * 256) {
+        const int2 ch = A.lchild[L][q];
+        if (ch.x < 0 && ch.y < 0) continue;
+        A.lcol[L][q] = accumulate(S, A.lcol[L][q], A.linfo[L][q], ch, A.lcol[L + 1]);
+    }
+}
+
+// Level 0 of the pixel's nine trees, the sum over sub-samples (:513-515) and
+// the x28 / clamp / XRGB pack (:517-523).
+__global__ void __launch_bounds__(256)
+final_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A, int row_end,
+             uint32_t *__restrict__ out)
+{
+    __shared__ Scene S;
+    stage_scene(S, prims, nprims);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int y = A.row_begin + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    if (x >= A.w || y >= row_end) return;
+    const int pix = (y - A.row_begin) * A.w + x;
+    float tr = 0.f, tg = 0.f, tb = 0.f;
+    for (int sub = 0; sub < 9; sub++) {
+        const int tree = sub * A.npix + pix;
+        float4 c0 = A.rcol[tree];
+        if (A.fixflag[tree] == 0) {
+            const int2 ch = A.rchild[tree];
+            if (ch.x >= 0 || ch.y >= 0) c0 = accumulate(S, c0, A.rinfo[tree], ch, A.lcol[1]);
+        }
+        tr += c0.x; tg += c0.y; tb += c0.z;
+    }
+    int red = (int)(tr * 28.0f), green = (int)(tg * 28.0f), blue = (int)(tb * 28.0f);
+    if (red > 255) red = 255;
+    if (green > 255) green = 255;
+    if (blue > 255) blue = 255;
+    out[(size_t)y * A.w + x] = (uint32_t)((red << 16) + (green << 8) + blue);
+}
+
+struct NodeStore {       // per-lane private tree records (only traced nodes touched)
+    float4 col[NODES];   // colour.xyz, dist
+    int info[NODES];     // hit primitive | INFO_TIR
+    float4 ra[NODES];    // refl ray o.xyz, d.x
+    float4 rb[NODES];    // refl ray d.yz, refr ray o.xy
+    float4 rc[NODES];    // refr ray o.z, d.xyz
+    float rin[NODES];    // *a_RIndex after the node's call
+    int wf[NODES];       // the node's record slot in the wavefront pass, -1 if it did not trace it
+};
+
+__device__ __forceinline__ int level_of(int i) { return 31 - __builtin_clz(i + 1); }
+
+// Sequential re-evaluation of flagged trees in the reference's BFS order: a
+// 64-bit to-do mask (ctz = next node; children 2i+1 / 2i+2 are always later)
+// and the caller's refr_Ray variable carried across nodes (cur_refr), so the
+// stale-ray quirk is reproduced; back-accumulation in decreasing index.
+// Writes the tree's final level-0 colour into rcol[tree].
+template <bool COUNT>
+__global__ void __launch_bounds__(64)
+fixup_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A,
+             const float *__restrict__ sx_tab, const float *__restrict__ sy_tab, float DX, float DY,
+             unsigned long long *__restrict__ counters)
+{
+    __shared__ Scene S;
+    stage_scene(S, prims, nprims);
+    const int nfix = A.count[LEVELS];
+    Counts cnt = {0, 0, 0, 0};
+    for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < nfix; f += gridDim.x * blockDim.x) {
+        const int tree = A.fixlist[f];
+        const int sub = tree / A.npix, pix = tree % A.npix;
+        const int x = pix % A.w, y = A.row_begin + pix / A.w;
         NodeStore ns;
-        float tr = 0.f, tg = 0.f, tb = 0.f;
-        int sub = 0;
         unsigned long long todo = 1, traced = 0;
-        ray3 root = primary(0, SX, SY, DX, DY);
-        ray3 cur_refr = root;              // the caller's refr_Ray variable (:373-374)
-        for (;;) {
+        const ray3 root = primary(sub, sx_tab[x], sy_tab[y], DX, DY);
+        ray3 cur_refr = root;          // the caller's refr_Ray variable (:373-374)
+        while (todo) {
             const int i = __builtin_ctzll(todo);
             todo &= todo - 1;
             traced |= 1ull << i;
             ray3 r;
             float rin;
+            int wf = -1;
             if (i == 0) {
-                r = root; rin = 1.0f;
+                r = root; rin = 1.0f; wf = tree;
             } else {
                 const int p = (i - 1) >> 1;
                 const float4 a = ns.ra[p], b = ns.rb[p], c = ns.rc[p];
                 if (i & 1) { r.o = mk(a.x, a.y, a.z); r.d = mk(a.w, b.x, b.y); }
                 else       { r.o = mk(b.z, b.w, c.x); r.d = mk(c.y, c.z, c.w); }
                 rin = ns.rin[p];
+                if (ns.wf[p] >= 0) {
+                    const int lp = level_of(p);
+                    const int2 ch = lp == 0 ? A.rchild[ns.wf[p]] : A.lchild[lp][ns.wf[p]];
+                    wf = (i & 1) ? ch.x : ch.y;
+                }
             }
-            Hit hh = trace(S, r, rin, cnt);
+            Counts c1 = {0, 0, 0, 0};
+            Hit hh = trace(S, r, rin, c1);
             const bool tir = hh.refr > 0 && !hh.refr_ray_ok;
+            if (wf < 0) {                  // not traced by the wavefront: count it here
+                cnt.traced += c1.traced; cnt.shadow += c1.shadow; cnt.tests += c1.tests;
+                if (tir && i < NODES / 2) cnt.tir++;
+            }
             ns.col[i] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
-            ns.info[i] = (hh.prim & 0xff) | (tir ? 0x100 : 0);
+            ns.info[i] = (hh.prim & 0xff) | (tir ? INFO_TIR : 0);
+            ns.wf[i] = wf;
             if (hh.refr_ray_ok) cur_refr = hh.refr_ray;
             if (i < NODES / 2) {
-                if (tir) cnt.tir++;
                 const bool cl = hh.refl > 0, cr = hh.refr > 0;
                 if (cl || cr) {
                     const ray3 fl = hh.refl_ray, fr = cur_refr;
@@ -390,48 +655,35 @@ render_kernel(const rt_primitive *__restrict__ prims, int nprims, uint32_t *__re
                     if (cr) todo |= 1ull << (2 * i + 2);
                 }
             }
-            if (todo) continue;
-            // Back-accumulation (:476-511): children in decreasing index order,
-            // refraction child (even) before reflection child (odd).
-            unsigned long long m = traced & ~1ull;
-            while (m) {
-                const int c = 63 - __builtin_clzll(m);
-                m &= ~(1ull << c);
-                const int p = (c - 1) >> 1;
-                const float4 cc = ns.col[c];
-                float4 pc = ns.col[p];
-                const int pinfo = ns.info[p];
-                const int pp = pinfo & 0xff;
-                const float4 pm = S.mat0[pp];
-                float ax = cc.x, ay = cc.y, az = cc.z;
-                if (!(c & 1)) {
-                    if (!(pinfo & 0x100)) {
-                        const float nd = -pc.w;
-                        ax = cc.x * rtm::expf(pm.x * 0.15f * nd);
-                        ay = cc.y * rtm::expf(pm.y * 0.15f * nd);
-                        az = cc.z * rtm::expf(pm.z * 0.15f * nd);
-                    }
-                } else {
-                    ax = cc.x * pm.x * pm.w;
-                    ay = cc.y * pm.y * pm.w;
-                    az = cc.z * pm.z * pm.w;
-                }
-                pc.x += ax; pc.y += ay; pc.z += az;
-                ns.col[p] = pc;
-            }
-            const float4 c0 = ns.col[0];
-            tr += c0.x; tg += c0.y; tb += c0.z;
-            if (++sub == 9) break;
-            root = primary(sub, SX, SY, DX, DY);
-            cur_refr = root;
-            todo = 1;
-            traced = 0;
         }
-        int red = (int)(tr * 28.0f), green = (int)(tg * 28.0f), blue = (int)(tb * 28.0f);
-        if (red > 255) red = 255;
-        if (green > 255) green = 255;
-        if (blue > 255) blue = 255;
-        out[(size_t)y * w + x] = (uint32_t)((red << 16) + (green << 8) + blue);
+        // Back-accumulation (:476-511): children in decreasing index order,
+        // refraction child (even) before reflection child (odd).
+        unsigned long long m = traced & ~1ull;
+        while (m) {
+            const int c = 63 - __builtin_clzll(m);
+            m &= ~(1ull << c);
+            const int p = (c - 1) >> 1;
+            const float4 cc = ns.col[c];
+            float4 pc = ns.col[p];
+            const int pinfo = ns.info[p];
+            const float4 pm = S.mat0[pinfo & 0xff];
+            float ax = cc.x, ay = cc.y, az = cc.z;
+            if (!(c & 1)) {
+                if (!(pinfo & INFO_TIR)) {
+                    const float nd = -pc.w;
+                    ax = cc.x * rtm::expf(pm.x * 0.15f * nd);
+                    ay = cc.y * rtm::expf(pm.y * 0.15f * nd);
+                    az = cc.z * rtm::expf(pm.z * 0.15f * nd);
+                }
+            } else {
+                ax = cc.x * pm.x * pm.w;
+                ay = cc.y * pm.y * pm.w;
+                az = cc.z * pm.z * pm.w;
+            }
+            pc.x += ax; pc.y += ay; pc.z += az;
+            ns.col[p] = pc;
+        }
+        A.rcol[tree] = ns.col[0];
     }
     if (COUNT) {
         const unsigned long long c[4] = {cnt.traced, cnt.shadow, cnt.tests, cnt.tir};
@@ -443,9 +695,13 @@ render_kernel(const rt_primitive *__restrict__ prims, int nprims, uint32_t *__re
 }  // namespace rt
 
 // ------------------------------------------------------------------ host side
+#include <stdlib.h>
+#include <algorithm>
 #include "rt_runtime.h"
 
 namespace {
+
+constexpr int SLOT_WF = 6;      // rtrt scratch slot of the wavefront arena
 
 // m_SX / m_SY tables (Engine_InitRender raytracer.cpp:278-294, then the
 // sequential m_SX += m_DX (:524) and m_SY += m_DY (:526)) -- host float adds,
@@ -476,6 +732,52 @@ int view_tables(rtrt::DeviceState &st, int w, int h, const float **d_sx, const f
     return RT_OK;
 }
 
+// Device arena of the wavefront pass (scratch slot SLOT_WF, grow-only):
+// per tree a root record, per level 1..5 a queue of capacity = #trees.
+int wavefront_arena(rtrt::DeviceState &st, int w, int rows, rt::whitted::WfArgs *A)
+{
+    using namespace rt::whitted;
+    const size_t T = (size_t)w * rows * 9;
+    if (T > (size_t)0x7fffffff / 2) return rtrt::fail(RT_ERR_INVALID, "rtw: frame too large");
+    // Queue capacity per level: one slot per tree.  RT_WHITTED_QUEUE_CAP
+    // lowers it (test hook: exercises the overflow -> fixup path).
+    size_t C = T;
+    if (const char *e = getenv("RT_WHITTED_QUEUE_CAP")) {
+        const long long v = atoll(e);
+        if (v > 0 && (size_t)v < C) C = (size_t)v;
+    }
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t root_b = al(T * 16) + al(T * 4) + al(T * 8) + al(T * 4) + al(T * 4);
+    const size_t lvl_b = al(C * 16) * 3 + al(C * 4) + al(C * 8);
+    const size_t bytes = root_b + (LEVELS - 1) * lvl_b + al(sizeof(int) * (LEVELS + 1));
+    void *base = nullptr;
+    int rc = rtrt::scratch(st, SLOT_WF, bytes, &base);
+    if (rc) return rc;
+    char *p = (char *)base;
+    auto take = [&](size_t b) { char *q = p; p += al(b); return q; };
+    A->rcol = (float4 *)take(T * 16);
+    A->rinfo = (int *)take(T * 4);
+    A->rchild = (int2 *)take(T * 8);
+    A->fixflag = (int *)take(T * 4);
+    A->fixlist = (int *)take(T * 4);
+    A->ia[0] = A->ib[0] = A->lcol[0] = nullptr;
+    A->linfo[0] = nullptr;
+    A->lchild[0] = nullptr;
+    for (int L = 1; L < LEVELS; L++) {
+        A->ia[L] = (float4 *)take(C * 16);
+        A->ib[L] = (float4 *)take(C * 16);
+        A->lcol[L] = (float4 *)take(C * 16);
+        A->linfo[L] = (int *)take(C * 4);
+        A->lchild[L] = (int2 *)take(C * 8);
+    }
+    A->count = (int *)take(sizeof(int) * (LEVELS + 1));
+    A->cap = (int)C;
+    A->ntrees = (int)T;
+    A->npix = w * rows;
+    A->w = w;
+    return RT_OK;
+}
+
 }  // namespace
 
 extern "C" int rtw_render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int w,
@@ -493,17 +795,39 @@ extern "C" int rtw_render_async(const rt_primitive *d_prims, int nprims, uint32_
     rc = view_tables(*st, w, h, &d_sx, &d_sy);
     if (rc) return rc;
     const int rows = row_end - row_begin;
-    dim3 grid((w + 15) / 16, (rows + 15) / 16), block(256);
+    rt::whitted::WfArgs A;
+    rc = wavefront_arena(*st, w, rows, &A);
+    if (rc) return rc;
+    A.row_begin = row_begin;
     hipStream_t s = (hipStream_t)stream;
-    if (d_counters)
-        hipLaunchKernelGGL(rt::whitted::render_kernel<true>, grid, block, 0, s, d_prims, nprims,
-                           d_xrgb, w, row_begin, row_end, d_sx, d_sy, st->vt_DX, st->vt_DY,
-                           (unsigned long long *)d_counters);
-    else
-        hipLaunchKernelGGL(rt::whitted::render_kernel<false>, grid, block, 0, s, d_prims, nprims,
-                           d_xrgb, w, row_begin, row_end, d_sx, d_sy, st->vt_DX, st->vt_DY,
-                           (unsigned long long *)nullptr);
-    return rtrt::check_launch("rtw render_kernel");
+    unsigned long long *cnt = (unsigned long long *)d_counters;
+    hipError_t e = hipMemsetAsync(A.count, 0, sizeof(int) * (rt::whitted::LEVELS + 1), s);
+    if (e == hipSuccess) e = hipMemsetAsync(A.fixflag, 0, sizeof(int) * (size_t)A.ntrees, s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async memset");
+    const dim3 tiles((w + 15) / 16, (rows + 15) / 16), block(256);
+    // Queue kernels: a fixed grid striding over the device-side queue length.
+    const int qblocks = (int)std::min<long long>(((long long)A.cap + 255) / 256, 2048);
+    if (cnt) {
+        hipLaunchKernelGGL(rt::whitted::root_kernel<true>, tiles, block, 0, s, d_prims, nprims, A, row_end,
+                           d_sx, d_sy, st->vt_DX, st->vt_DY, cnt);
+        for (int L = 1; L < rt::whitted::LEVELS; L++)
+            hipLaunchKernelGGL(rt::whitted::level_kernel<true>, dim3(qblocks), block, 0, s, d_prims, nprims, A,
+                               L, cnt);
+        hipLaunchKernelGGL(rt::whitted::fixup_kernel<true>, dim3(256), dim3(64), 0, s, d_prims, nprims, A,
+                           d_sx, d_sy, st->vt_DX, st->vt_DY, cnt);
+    } else {
+        hipLaunchKernelGGL(rt::whitted::root_kernel<false>, tiles, block, 0, s, d_prims, nprims, A, row_end,
+                           d_sx, d_sy, st->vt_DX, st->vt_DY, cnt);
+        for (int L = 1; L < rt::whitted::LEVELS; L++)
+            hipLaunchKernelGGL(rt::whitted::level_kernel<false>, dim3(qblocks), block, 0, s, d_prims, nprims,
+                               A, L, cnt);
+        hipLaunchKernelGGL(rt::whitted::fixup_kernel<false>, dim3(256), dim3(64), 0, s, d_prims, nprims, A,
+                           d_sx, d_sy, st->vt_DX, st->vt_DY, cnt);
+    }
+    for (int L = rt::whitted::LEVELS - 2; L >= 1; L--)
+        hipLaunchKernelGGL(rt::whitted::backacc_kernel, dim3(qblocks), block, 0, s, d_prims, nprims, A, L);
+    hipLaunchKernelGGL(rt::whitted::final_kernel, tiles, block, 0, s, d_prims, nprims, A, row_end, d_xrgb);
+    return rtrt::check_launch("rtw wavefront kernels");
 }
 
 extern "C" int rtw_render(const rt_primitive *prims, int nprims, uint32_t *xrgb, int w, int h,

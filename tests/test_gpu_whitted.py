@@ -46,3 +46,22 @@ def test_golden_hashes(rt, oracle):
         w, h = map(int, key.split("x"))
         f, c = rt.whitted_render(w, h, counters=True)
         assert oracle.fnv1a64(f) == g["xrgb"] and c == g["counters"], key
+
+
+@pytest.mark.parametrize("cap", [1, 1000, 20000])
+def test_queue_overflow_falls_back_exactly(rt, oracle, cap, monkeypatch):
+    # Child queues smaller than the tree count: nodes that do not fit are
+    # evaluated by the sequential fixup pass; frame and counts stay exact.
+    monkeypatch.setenv("RT_WHITTED_QUEUE_CAP", str(cap))
+    w, h = 320, 240
+    ref, rc = oracle.whitted_render(w, h, nthreads=8)
+    got, gc = rt.whitted_render(w, h, counters=True)
+    assert (got == ref).all() and gc == rc
+
+
+def test_tir_trees_counted_once(rt, oracle):
+    # 640x480 holds 1,874 total-internal-reflection events:
+    # their trees go through the fixup pass; the TIR count must match.
+    _, rc = oracle.whitted_render(640, 480, nthreads=8)
+    _, gc = rt.whitted_render(640, 480, counters=True)
+    assert rc[3] == 1874 and gc == rc

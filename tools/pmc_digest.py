@@ -18,13 +18,13 @@ dur = defaultdict(list)
 for f in sorted(glob.glob(os.path.join(root, "pmc*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        if "render_kernel" not in name:
+        if "rt::smallpt::" not in name and "rt::whitted::" not in name:
             continue
         key = name.split("(")[0].replace("void ", "")
         acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for f in sorted(glob.glob(os.path.join(root, "stats", "*kernel_stats.csv"))):
     for r in csv.DictReader(open(f)):
-        if "render_kernel" in r["Name"]:
+        if "rt::smallpt::" in r["Name"] or "rt::whitted::" in r["Name"]:
             dur[r["Name"].split("(")[0].replace("void ", "")].append(float(r["AverageNs"]))
 out = {}
 for k, c in acc.items():
