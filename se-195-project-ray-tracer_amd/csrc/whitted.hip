@@ -59,6 +59,7 @@ struct Scene {
     int light[MAXP];
     int lights[MAXP];   // indices of m_Light > 0 primitives, in index order
     int n, nnonlight, nlights;
+    int pad_;                                     // sizeof(Scene) % 16 == 0
 };
 
 // Sphere half of Primitive_Intersect (scene.cpp:130-169): the candidate
@@ -288,8 +289,9 @@ __device__ __forceinline__ ray3 primary(int sub, float SX, float SY, float DX, f
     return r;
 }
 
-// Stages the reference's 96-byte AoS primitives into the block's LDS SoA.
-__device__ void stage_scene(Scene &S, const rt_primitive *__restrict__ prims, int nprims)
+// Builds the SoA scene image from the reference's 96-byte AoS primitives
+// (one block; scene_kernel writes it to the frame's arena once per render).
+__device__ void build_scene(Scene &S, const rt_primitive *__restrict__ prims, int nprims)
 {
     for (int p = threadIdx.x; p < nprims; p += blockDim.x) {
         const rt_primitive &q = prims[p];
@@ -323,6 +325,21 @@ __device__ void stage_scene(Scene &S, const rt_primitive *__restrict__ prims, in
         S.n = nprims; S.nlights = nl; S.nnonlight = nn;
         S.ns = ns; S.np = np; S.nos = nos; S.nop = nop;
     }
+}
+
+__global__ void __launch_bounds__(64) scene_kernel(const rt_primitive *__restrict__ prims, int nprims,
+                                                   Scene *__restrict__ out)
+{
+    build_scene(*out, prims, nprims);
+}
+
+// Block-cooperative copy of the scene image into LDS (coalesced 16-B loads).
+__device__ __forceinline__ void load_scene(Scene &S, const Scene *__restrict__ g)
+{
+    static_assert(sizeof(Scene) % 16 == 0, "Scene image is copied in 16-B words");
+    const uint4 *src = (const uint4 *)g;
+    uint4 *dst = (uint4 *)&S;
+    for (int i = threadIdx.x; i < (int)(sizeof(Scene) / 16); i += blockDim.x) dst[i] = src[i];
     __syncthreads();
 }
 
@@ -354,27 +371,43 @@ __device__ void stage_scene(Scene &S, const rt_primitive *__restrict__ prims, in
 // The fixup counts only the nodes the wavefront did not trace, so counters
 // stay exactly the reference's.
 constexpr int LEVELS = 6;
-constexpr int INFO_TIR = 0x100;
+constexpr int INFO_TIR = 0x100;       // refr > 0 but no refraction ray (TIR)
+constexpr int INFO_REFR_OK = 0x200;   // the node wrote a refraction ray
+// Each level's queue is split into NSEG segments with their own counters: a
+// producing wave appends to segment (wave id mod NSEG), so thousands of
+// waves finishing a step together do not queue on one atomic address.
+constexpr int NSEG = 64;
+// count[] layout (zeroed per frame).  Every counter has its own 128-B line
+// (same-line atomics serialise in the L2's atomic unit).
+constexpr int CSTRIDE = 32;
+constexpr int C_FIX = 0;                      // fixup list length
+constexpr int C_TIR = 1;                      // + L: TIR list length of level L (0..4)
+constexpr int C_SEG = C_TIR + LEVELS;         // + L * NSEG + s: length of segment s of level L (1..5)
+constexpr int C_TOTAL = C_SEG + LEVELS * NSEG;
+#define CNT(A, i) ((A).count[(i) * CSTRIDE])
 
 struct WfArgs {
+    const Scene *scene;       // scene image (scene_kernel)
     float4 *rcol;             // [ntrees] root colour.xyz, dist
-    int *rinfo;               // [ntrees] hit primitive | INFO_TIR
+    int *rinfo;               // [ntrees] hit primitive | INFO_*
     int2 *rchild;             // [ntrees] queue slots (level 1) of refl / refr child, -1 if none
     int *fixflag;             // [ntrees] 0, or -1 once queued for fixup
     int *fixlist;             // [ntrees] trees to fix
     float4 *ia[LEVELS];       // [cap] queued ray: o.xyz, d.x
     float4 *ib[LEVELS];       // [cap] d.y, d.z, rindex, tree (int bits)
+    int *lnode[LEVELS];       // [cap] the node's index in the reference's 63-slot array
     float4 *lcol[LEVELS];     // [cap] node colour.xyz, dist
-    int *linfo[LEVELS];       // [cap] hit primitive | INFO_TIR
+    int *linfo[LEVELS];       // [cap] hit primitive | INFO_*
     int2 *lchild[LEVELS];     // [cap] child slots in level L+1
-    int *count;               // [LEVELS] queue lengths (index 1..5), [LEVELS] fixup count
-    int cap, ntrees, npix, w, row_begin;
+    int4 *tir[LEVELS];        // [tcap] TIR nodes of level L: slot, tree, node, rindex (bits)
+    int *count;               // [C_TOTAL * CSTRIDE]
+    int cap, segcap, tcap, ntrees, npix, w, row_begin;   // cap = NSEG * segcap
 };
 
 __device__ void flag_tree(const WfArgs &A, int tree)
 {
     if (atomicCAS(&A.fixflag[tree], 0, -1) == 0) {
-        const int s = atomicAdd(&A.count[LEVELS], 1);
+        const int s = atomicAdd(&CNT(A, C_FIX), 1);
         A.fixlist[s] = tree;
     }
 }
@@ -396,49 +429,95 @@ __device__ __forceinline__ int wave_alloc(int *counter, int want)
     return base + pre;
 }
 
-// Queues the children of a just-traced node (level L < 5) into level L+1 and
-// returns their slots (-1: not queued).  All lanes of the wave call it.
-__device__ __forceinline__ int2 queue_children(const WfArgs &A, int L, bool active, int tree, const Hit &hh,
-                                               bool tir)
+__device__ __forceinline__ void put_item(const WfArgs &A, int L, int slot, const ray3 &r, float rin, int tree,
+                                         int node)
+{
+    A.ia[L][slot] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+    A.ib[L][slot] = make_float4(r.d.y, r.d.z, rin, __int_as_float(tree));
+    A.lnode[L][slot] = node;
+}
+
+// Queues the children of node `node` (level L < 5, record `slot`) into level
+// L+1 and returns their slots (-1: not queued).  A TIR node's refraction child
+// is queued later by tir_kernel, once every node before it in BFS order has
+// been traced.  All lanes of the wave call it.
+__device__ __forceinline__ int2 queue_children(const WfArgs &A, int L, int wave_id, bool active, int slot_self,
+                                               int tree, int node, const Hit &hh, bool tir)
 {
     const bool cl = active && hh.refl > 0, cr = active && hh.refr > 0;
     const bool qr = cr && !tir;
-    int slot = wave_alloc(&A.count[L + 1], (int)cl + (int)qr);
+    const int seg = wave_id & (NSEG - 1);
+    int slot = wave_alloc(&CNT(A, C_SEG + (L + 1) * NSEG + seg), (int)cl + (int)qr);
     int2 ch = make_int2(-1, -1);
     if (cl) {
-        if (slot < A.cap) {
-            const ray3 &r = hh.refl_ray;
-            A.ia[L + 1][slot] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-            A.ib[L + 1][slot] = make_float4(r.d.y, r.d.z, hh.rindex_out, __int_as_float(tree));
-            ch.x = slot;
+        if (slot < A.segcap) {
+            put_item(A, L + 1, seg * A.segcap + slot, hh.refl_ray, hh.rindex_out, tree, 2 * node + 1);
+            ch.x = seg * A.segcap + slot;
         } else {
             flag_tree(A, tree);
         }
         slot++;
     }
-    if (cr) {
-        if (tir) {
-            flag_tree(A, tree);
-        } else if (slot < A.cap) {
-            const ray3 &r = hh.refr_ray;
-            A.ia[L + 1][slot] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-            A.ib[L + 1][slot] = make_float4(r.d.y, r.d.z, hh.rindex_out, __int_as_float(tree));
-            ch.y = slot;
+    if (qr) {
+        if (slot < A.segcap) {
+            put_item(A, L + 1, seg * A.segcap + slot, hh.refr_ray, hh.rindex_out, tree, 2 * node + 2);
+            ch.y = seg * A.segcap + slot;
         } else {
             flag_tree(A, tree);
         }
     }
+    if (cr && tir) {
+        const int t = atomicAdd(&CNT(A, C_TIR + L), 1);
+        if (t < A.tcap) A.tir[L][t] = make_int4(slot_self, tree, node, __float_as_int(hh.rindex_out));
+        else flag_tree(A, tree);
+    }
     return ch;
+}
+
+__device__ __forceinline__ int node_info(const Hit &hh, bool tir)
+{
+    return (hh.prim & 0xff) | (tir ? INFO_TIR : 0) | (hh.refr_ray_ok ? INFO_REFR_OK : 0);
+}
+
+// Consumer view of level L's segmented queue: lane s holds segment s's length
+// and the inclusive prefix of its 64-item chunk counts.  Whole waves only.
+struct SegView { int incl, n; };
+
+__device__ __forceinline__ SegView seg_view(const WfArgs &A, int L)
+{
+    const int lane = __lane_id();
+    SegView v;
+    v.n = min(CNT(A, C_SEG + L * NSEG + lane), A.segcap);
+    int x = (v.n + 63) >> 6;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    v.incl = x;
+    return v;
+}
+
+// Chunk k (wave-uniform) of the queue: first slot and number of valid items;
+// false once k is past the last chunk.
+__device__ __forceinline__ bool seg_chunk(const WfArgs &A, const SegView &v, int k, int &base, int &nvalid)
+{
+    if (k >= __shfl(v.incl, 63, 64)) return false;
+    const int s = __popcll(__builtin_amdgcn_ballot_w64(v.incl <= k));
+    const int incl = __shfl(v.incl, s, 64), n = __shfl(v.n, s, 64);
+    const int c = k - (incl - ((n + 63) >> 6));
+    base = s * A.segcap + c * 64;
+    nvalid = min(64, n - c * 64);
+    return true;
 }
 
 template <bool COUNT>
 __global__ void __launch_bounds__(256)
-root_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A, int row_end,
-            const float *__restrict__ sx_tab, const float *__restrict__ sy_tab, float DX, float DY,
-            unsigned long long *__restrict__ counters)
+root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float *__restrict__ sy_tab,
+            float DX, float DY, unsigned long long *__restrict__ counters)
 {
     __shared__ Scene S;
-    stage_scene(S, prims, nprims);
+    load_scene(S, A.scene);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int y = A.row_begin + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
@@ -455,10 +534,11 @@ root_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A, int ro
             if (tir) cnt.tir++;
         }
         const int tree = sub * A.npix + pix;
-        const int2 ch = queue_children(A, 0, active, tree, hh, tir);
+        const int wave_id = ((blockIdx.y * gridDim.x + blockIdx.x) << 2) + wave;
+        const int2 ch = queue_children(A, 0, wave_id, active, tree, tree, 0, hh, tir);
         if (active) {
             A.rcol[tree] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
-            A.rinfo[tree] = (hh.prim & 0xff) | (tir ? INFO_TIR : 0);
+            A.rinfo[tree] = node_info(hh, tir);
             A.rchild[tree] = ch;
         }
     }
@@ -468,23 +548,28 @@ root_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A, int ro
     }
 }
 
+// Level L = 1..5: a grid of resident blocks; wave w takes 64-ray chunks
+// w, w + #waves, ... of the level's queue.
 template <bool COUNT>
 __global__ void __launch_bounds__(256)
-level_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A, int L,
-             unsigned long long *__restrict__ counters)
+level_kernel(WfArgs A, int L, unsigned long long *__restrict__ counters)
 {
     __shared__ Scene S;
-    stage_scene(S, prims, nprims);
-    const int n = min(A.count[L], A.cap);
+    load_scene(S, A.scene);
+    const SegView v = seg_view(A, L);
+    const int lane = __lane_id();
+    const int wave_id = (blockIdx.x << 2) + (threadIdx.x >> 6);
     Counts cnt = {0, 0, 0, 0};
-    for (int base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {   // block-uniform trip count
-        const int q = base + threadIdx.x;
-        const bool active = q < n;
+    int base, nvalid;
+    for (int k = wave_id; seg_chunk(A, v, k, base, nvalid); k += gridDim.x << 2) {
+        const int q = base + lane;
+        const bool active = lane < nvalid;
         Hit hh;
         bool tir = false;
-        int tree = 0;
+        int tree = 0, node = 0;
         if (active) {
             const float4 a = A.ia[L][q], b = A.ib[L][q];
+            node = A.lnode[L][q];
             ray3 r;
             r.o = mk(a.x, a.y, a.z);
             r.d = mk(a.w, b.x, b.y);
@@ -493,16 +578,78 @@ level_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A, int L
             tir = hh.refr > 0 && !hh.refr_ray_ok;
             if (tir && L < 5) cnt.tir++;                // node index < 31 (:398)
             A.lcol[L][q] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
-            A.linfo[L][q] = (hh.prim & 0xff) | (tir ? INFO_TIR : 0);
+            A.linfo[L][q] = node_info(hh, tir);
         }
         if (L < 5) {
-            const int2 ch = queue_children(A, L, active, tree, hh, tir);
+            const int2 ch = queue_children(A, L, wave_id, active, q, tree, node, hh, tir);
             if (active) A.lchild[L][q] = ch;
         }
     }
     if (COUNT) {
         const unsigned long long c[4] = {cnt.traced, cnt.shadow, cnt.tests, cnt.tir};
         flush_counters<4>(counters, c);
+    }
+}
+
+// Record of node `j` of `tree`, walking the child links from the root
+// (heap position j+1: after its leading 1, bit 0 = reflection child, bit 1 =
+// refraction child).  Returns false if the node was not traced.
+__device__ bool find_node(const WfArgs &A, int tree, int j, int &lvl, int &slot)
+{
+    const unsigned h = (unsigned)j + 1u;
+    const int depth = 31 - __builtin_clz(h);
+    slot = tree;
+    lvl = 0;
+    for (int k = depth - 1; k >= 0; k--) {
+        const int2 ch = lvl == 0 ? A.rchild[slot] : A.lchild[lvl][slot];
+        slot = ((h >> k) & 1u) ? ch.y : ch.x;
+        lvl++;
+        if (slot < 0) return false;
+    }
+    return true;
+}
+
+// TIR nodes of level L (0..4): the reference traces their refraction child
+// with its refr_Ray variable as the previous calls left it -- the refraction
+// ray of the last node before this one in BFS order that wrote one, or the
+// primary ray (raytracer.cpp:231-233, :373-374, :412).  Every node before it
+// has been traced by now (levels <= L); queue that child into level L+1.
+__global__ void __launch_bounds__(64)
+tir_kernel(WfArgs A, int L, const float *__restrict__ sx_tab, const float *__restrict__ sy_tab, float DX,
+           float DY)
+{
+    const int nt = min(CNT(A, C_TIR + L), A.tcap);
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+        const int4 e = A.tir[L][t];
+        const int slot_self = e.x, tree = e.y, node = e.z;
+        const float rin = __int_as_float(e.w);
+        ray3 r;
+        bool found = false, broken = false;
+        for (int j = node - 1; j >= 0 && !found && !broken; j--) {
+            int lv, sl;
+            if (!find_node(A, tree, j, lv, sl)) continue;
+            const int info = lv == 0 ? A.rinfo[sl] : A.linfo[lv][sl];
+            if (!(info & INFO_REFR_OK)) continue;
+            const int c = (lv == 0 ? A.rchild[sl] : A.lchild[lv][sl]).y;   // its own refraction child
+            if (c < 0) { broken = true; break; }                          // not queued (overflow)
+            const float4 a = A.ia[lv + 1][c], b = A.ib[lv + 1][c];
+            r.o = mk(a.x, a.y, a.z);
+            r.d = mk(a.w, b.x, b.y);
+            found = true;
+        }
+        if (broken) { flag_tree(A, tree); continue; }
+        if (!found) {
+            const int sub = tree / A.npix, pix = tree % A.npix;
+            const int x = pix % A.w, y = A.row_begin + pix / A.w;
+            r = primary(sub, sx_tab[x], sy_tab[y], DX, DY);
+        }
+        const int seg = tree & (NSEG - 1);
+        const int k = atomicAdd(&CNT(A, C_SEG + (L + 1) * NSEG + seg), 1);
+        if (k >= A.segcap) { flag_tree(A, tree); continue; }
+        const int q = seg * A.segcap + k;
+        put_item(A, L + 1, q, r, rin, tree, 2 * node + 2);
+        if (L == 0) A.rchild[slot_self].y = q;
+        else A.lchild[L][slot_self].y = q;
     }
 }
 
@@ -534,12 +681,16 @@ __device__ __forceinline__ float4 accumulate(const Scene &S, float4 pc, int pinf
 }
 
 __global__ void __launch_bounds__(256)
-backacc_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A, int L)
+backacc_kernel(WfArgs A, int L)
 {
     __shared__ Scene S;
-    stage_scene(S, prims, nprims);
-    const int n = min(A.count[L], A.cap);
-    for (int q = blockIdx.x * 256 + threadIdx.x; q < n; q += gridDim.x * 256) {
+    load_scene(S, A.scene);
+    const SegView v = seg_view(A, L);
+    const int lane = __lane_id();
+    int base, nvalid;
+    for (int k = (blockIdx.x << 2) + (threadIdx.x >> 6); seg_chunk(A, v, k, base, nvalid); k += gridDim.x << 2) {
+        const int q = base + lane;
+        if (lane >= nvalid) continue;
         const int2 ch = A.lchild[L][q];
         if (ch.x < 0 && ch.y < 0) continue;
         A.lcol[L][q] = accumulate(S, A.lcol[L][q], A.linfo[L][q], ch, A.lcol[L + 1]);
@@ -549,11 +700,10 @@ backacc_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A, int
 // Level 0 of the pixel's nine trees, the sum over sub-samples (:513-515) and
 // the x28 / clamp / XRGB pack (:517-523).
 __global__ void __launch_bounds__(256)
-final_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A, int row_end,
-             uint32_t *__restrict__ out)
+final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
 {
     __shared__ Scene S;
-    stage_scene(S, prims, nprims);
+    load_scene(S, A.scene);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int y = A.row_begin + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
@@ -588,20 +738,20 @@ struct NodeStore {       // per-lane private tree records (only traced nodes tou
 
 __device__ __forceinline__ int level_of(int i) { return 31 - __builtin_clz(i + 1); }
 
-// Sequential re-evaluation of flagged trees in the reference's BFS order: a
-// 64-bit to-do mask (ctz = next node; children 2i+1 / 2i+2 are always later)
-// and the caller's refr_Ray variable carried across nodes (cur_refr), so the
-// stale-ray quirk is reproduced; back-accumulation in decreasing index.
-// Writes the tree's final level-0 colour into rcol[tree].
+// Sequential re-evaluation, in the reference's BFS order, of trees the level
+// pass could not finish (a full queue): a 64-bit to-do mask (ctz = next node;
+// children 2i+1 / 2i+2 are always later), the caller's refr_Ray variable
+// carried across nodes (cur_refr), back-accumulation in decreasing index.
+// Writes the tree's final level-0 colour into rcol[tree]; counts only the
+// nodes the level pass did not trace.
 template <bool COUNT>
 __global__ void __launch_bounds__(64)
-fixup_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A,
-             const float *__restrict__ sx_tab, const float *__restrict__ sy_tab, float DX, float DY,
+fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict__ sy_tab, float DX, float DY,
              unsigned long long *__restrict__ counters)
 {
     __shared__ Scene S;
-    stage_scene(S, prims, nprims);
-    const int nfix = A.count[LEVELS];
+    load_scene(S, A.scene);
+    const int nfix = CNT(A, C_FIX);
     Counts cnt = {0, 0, 0, 0};
     for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < nfix; f += gridDim.x * blockDim.x) {
         const int tree = A.fixlist[f];
@@ -635,7 +785,7 @@ fixup_kernel(const rt_primitive *__restrict__ prims, int nprims, WfArgs A,
             Counts c1 = {0, 0, 0, 0};
             Hit hh = trace(S, r, rin, c1);
             const bool tir = hh.refr > 0 && !hh.refr_ray_ok;
-            if (wf < 0) {                  // not traced by the wavefront: count it here
+            if (wf < 0) {                  // not traced by the level pass: count it here
                 cnt.traced += c1.traced; cnt.shadow += c1.shadow; cnt.tests += c1.tests;
                 if (tir && i < NODES / 2) cnt.tir++;
             }
@@ -746,36 +896,74 @@ int wavefront_arena(rtrt::DeviceState &st, int w, int rows, rt::whitted::WfArgs 
         const long long v = atoll(e);
         if (v > 0 && (size_t)v < C) C = (size_t)v;
     }
+    const size_t SC = (C + NSEG - 1) / NSEG;           // per-segment capacity
+    C = SC * NSEG;
+    const size_t TC = std::max<size_t>(C / 8, 1024);    // TIR list per level
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t root_b = al(T * 16) + al(T * 4) + al(T * 8) + al(T * 4) + al(T * 4);
-    const size_t lvl_b = al(C * 16) * 3 + al(C * 4) + al(C * 8);
-    const size_t bytes = root_b + (LEVELS - 1) * lvl_b + al(sizeof(int) * (LEVELS + 1));
+    const size_t lvl_b = al(C * 16) * 3 + al(C * 4) * 2 + al(C * 8) + al(TC * 16);
+    const size_t bytes = al(sizeof(Scene)) + root_b + LEVELS * lvl_b + al(sizeof(int) * C_TOTAL * CSTRIDE);
     void *base = nullptr;
     int rc = rtrt::scratch(st, SLOT_WF, bytes, &base);
     if (rc) return rc;
     char *p = (char *)base;
     auto take = [&](size_t b) { char *q = p; p += al(b); return q; };
+    A->scene = (const Scene *)take(sizeof(Scene));
     A->rcol = (float4 *)take(T * 16);
     A->rinfo = (int *)take(T * 4);
     A->rchild = (int2 *)take(T * 8);
     A->fixflag = (int *)take(T * 4);
     A->fixlist = (int *)take(T * 4);
-    A->ia[0] = A->ib[0] = A->lcol[0] = nullptr;
-    A->linfo[0] = nullptr;
-    A->lchild[0] = nullptr;
-    for (int L = 1; L < LEVELS; L++) {
+    for (int L = 0; L < LEVELS; L++) {            // level 0 uses only its TIR list
         A->ia[L] = (float4 *)take(C * 16);
         A->ib[L] = (float4 *)take(C * 16);
         A->lcol[L] = (float4 *)take(C * 16);
+        A->lnode[L] = (int *)take(C * 4);
         A->linfo[L] = (int *)take(C * 4);
         A->lchild[L] = (int2 *)take(C * 8);
+        A->tir[L] = (int4 *)take(TC * 16);
     }
-    A->count = (int *)take(sizeof(int) * (LEVELS + 1));
+    A->count = (int *)take(sizeof(int) * C_TOTAL * CSTRIDE);
     A->cap = (int)C;
+    A->segcap = (int)SC;
+    A->tcap = (int)TC;
     A->ntrees = (int)T;
     A->npix = w * rows;
     A->w = w;
     return RT_OK;
+}
+
+// Resident blocks of a 256-thread kernel on this device (persistent grids).
+template <class K>
+int resident_blocks(K kernel)
+{
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 1024;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per < 1) per = 1;
+    return cus * per;
+}
+
+template <bool COUNT>
+int launch_wavefront(const rt_primitive *d_prims, int nprims, const rt::whitted::WfArgs &A, int w, int rows,
+                     int row_end, const float *d_sx, const float *d_sy, float DX, float DY,
+                     unsigned long long *cnt, hipStream_t s, uint32_t *d_xrgb)
+{
+    using namespace rt::whitted;
+    static const int level_blocks = resident_blocks(level_kernel<COUNT>);
+    const dim3 tiles((w + 15) / 16, (rows + 15) / 16), block(256);
+    const int qblocks = (int)std::min<long long>(((long long)A.cap + 255) / 256, 2048);
+    hipLaunchKernelGGL(scene_kernel, dim3(1), dim3(64), 0, s, d_prims, nprims, (Scene *)A.scene);
+    hipLaunchKernelGGL(root_kernel<COUNT>, tiles, block, 0, s, A, row_end, d_sx, d_sy, DX, DY, cnt);
+    for (int L = 1; L < LEVELS; L++) {
+        hipLaunchKernelGGL(tir_kernel, dim3(64), dim3(64), 0, s, A, L - 1, d_sx, d_sy, DX, DY);
+        hipLaunchKernelGGL(level_kernel<COUNT>, dim3(level_blocks), block, 0, s, A, L, cnt);
+    }
+    hipLaunchKernelGGL(fixup_kernel<COUNT>, dim3(256), dim3(64), 0, s, A, d_sx, d_sy, DX, DY, cnt);
+    for (int L = LEVELS - 2; L >= 1; L--)
+        hipLaunchKernelGGL(backacc_kernel, dim3(qblocks), block, 0, s, A, L);
+    hipLaunchKernelGGL(final_kernel, tiles, block, 0, s, A, row_end, d_xrgb);
+    return rtrt::check_launch("rtw wavefront kernels");
 }
 
 }  // namespace
@@ -801,33 +989,13 @@ extern "C" int rtw_render_async(const rt_primitive *d_prims, int nprims, uint32_
     A.row_begin = row_begin;
     hipStream_t s = (hipStream_t)stream;
     unsigned long long *cnt = (unsigned long long *)d_counters;
-    hipError_t e = hipMemsetAsync(A.count, 0, sizeof(int) * (rt::whitted::LEVELS + 1), s);
+    hipError_t e = hipMemsetAsync(A.count, 0, sizeof(int) * rt::whitted::C_TOTAL * rt::whitted::CSTRIDE, s);
     if (e == hipSuccess) e = hipMemsetAsync(A.fixflag, 0, sizeof(int) * (size_t)A.ntrees, s);
     if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async memset");
-    const dim3 tiles((w + 15) / 16, (rows + 15) / 16), block(256);
-    // Queue kernels: a fixed grid striding over the device-side queue length.
-    const int qblocks = (int)std::min<long long>(((long long)A.cap + 255) / 256, 2048);
-    if (cnt) {
-        hipLaunchKernelGGL(rt::whitted::root_kernel<true>, tiles, block, 0, s, d_prims, nprims, A, row_end,
-                           d_sx, d_sy, st->vt_DX, st->vt_DY, cnt);
-        for (int L = 1; L < rt::whitted::LEVELS; L++)
-            hipLaunchKernelGGL(rt::whitted::level_kernel<true>, dim3(qblocks), block, 0, s, d_prims, nprims, A,
-                               L, cnt);
-        hipLaunchKernelGGL(rt::whitted::fixup_kernel<true>, dim3(256), dim3(64), 0, s, d_prims, nprims, A,
-                           d_sx, d_sy, st->vt_DX, st->vt_DY, cnt);
-    } else {
-        hipLaunchKernelGGL(rt::whitted::root_kernel<false>, tiles, block, 0, s, d_prims, nprims, A, row_end,
-                           d_sx, d_sy, st->vt_DX, st->vt_DY, cnt);
-        for (int L = 1; L < rt::whitted::LEVELS; L++)
-            hipLaunchKernelGGL(rt::whitted::level_kernel<false>, dim3(qblocks), block, 0, s, d_prims, nprims,
-                               A, L, cnt);
-        hipLaunchKernelGGL(rt::whitted::fixup_kernel<false>, dim3(256), dim3(64), 0, s, d_prims, nprims, A,
-                           d_sx, d_sy, st->vt_DX, st->vt_DY, cnt);
-    }
-    for (int L = rt::whitted::LEVELS - 2; L >= 1; L--)
-        hipLaunchKernelGGL(rt::whitted::backacc_kernel, dim3(qblocks), block, 0, s, d_prims, nprims, A, L);
-    hipLaunchKernelGGL(rt::whitted::final_kernel, tiles, block, 0, s, d_prims, nprims, A, row_end, d_xrgb);
-    return rtrt::check_launch("rtw wavefront kernels");
+    if (cnt) return launch_wavefront<true>(d_prims, nprims, A, w, rows, row_end, d_sx, d_sy, st->vt_DX, st->vt_DY,
+                                           cnt, s, d_xrgb);
+    return launch_wavefront<false>(d_prims, nprims, A, w, rows, row_end, d_sx, d_sy, st->vt_DX, st->vt_DY, cnt,
+                                   s, d_xrgb);
 }
 
 extern "C" int rtw_render(const rt_primitive *prims, int nprims, uint32_t *xrgb, int w, int h,

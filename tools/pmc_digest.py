@@ -15,14 +15,14 @@ SIMDS, CLOCK_HZ = 1024, 2.4e9        # 256 CUs x 4 SIMDs, MI355X_MICROARCH.md
 root = sys.argv[1]
 acc = defaultdict(lambda: defaultdict(list))
 dur = defaultdict(list)
-for f in sorted(glob.glob(os.path.join(root, "pmc*", "*counter_collection.csv"))):
+for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
         if "rt::smallpt::" not in name and "rt::whitted::" not in name:
             continue
         key = name.split("(")[0].replace("void ", "")
         acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
-for f in sorted(glob.glob(os.path.join(root, "stats", "*kernel_stats.csv"))):
+for f in sorted(glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
         if "rt::smallpt::" in r["Name"] or "rt::whitted::" in r["Name"]:
             dur[r["Name"].split("(")[0].replace("void ", "")].append(float(r["AverageNs"]))
