@@ -13,7 +13,7 @@ import ctypes as C
 
 import numpy as np
 
-from . import scenes
+from . import ppm, scenes
 from ._lib import (Camera, Primitive, RTError, Sphere, Vec3, check, device_count, lib,
                    set_device, SPT_DIRECT_LIGHTING, SPT_PATH_TRACING)
 

@@ -1,0 +1,44 @@
+"""Times BASELINE configs[4] (10k-sphere scene_build_complex scene, 1920x1080)
+on one GPU: SPP samples per launch (default 1), HIP events; prints rays/s."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "se-195-project-ray-tracer_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import rtamd  # noqa: E402
+
+W, H = 1920, 1080
+SPP = int(os.environ.get("SPP", "1"))
+dev = torch.device("cuda", 0)
+spheres, n, cam = rtamd.scenes.complex10k()
+rtamd.scenes.update_camera(cam, W, H)
+sc = rtamd.SmallptScene(spheres, n)
+seeds0 = torch.from_numpy(rtamd.scenes.seeds(W, H).view(np.int32)).to(dev)
+seeds = torch.empty_like(seeds0)
+col = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
+px = torch.zeros(W * H, dtype=torch.int32, device=dev)
+cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+st = torch.cuda.current_stream(dev)
+L = rtamd.lib()
+
+
+def run(c=None):
+    rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                         seeds.data_ptr(), px.data_ptr(), W, H, 0, H, 0, SPP, 0,
+                                         c.data_ptr() if c is not None else None, st.cuda_stream))
+
+
+run(cnt)
+torch.cuda.synchronize()
+rays = int(cnt[0] + cnt[1])
+a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+a.record(st)
+run()
+b.record(st)
+torch.cuda.synchronize()
+ms = a.elapsed_time(b)
+print("c5 %dx%d spp=%d spheres=%d: %.1f ms, rays %d, %.1f Mrays/s, sphere tests %d" % (
+    W, H, SPP, n, ms, rays, rays / ms / 1e3, int(cnt[2])))
