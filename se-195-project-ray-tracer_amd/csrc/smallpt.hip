@@ -109,6 +109,105 @@ __device__ __forceinline__ int query(const G &geo, const ray3 &r, float &t, int 
     return id;
 }
 
+// ---------------------------------------------------------------------------
+// Bounding-volume hierarchy for large scenes (BASELINE configs[4]: 10k
+// spheres).  The reference tests every sphere for every ray (geomfunc.h:71-
+// 110); the result is the minimum over spheres of the float distance d_i of
+// SphereIntersect, ties to the highest index (Intersect), or "some d_i <
+// maxt" (IntersectP).  Both are order-independent, so a traversal that
+// computes d_i with the reference's exact float formula for every sphere it
+// visits, and skips a sphere only when d_i provably cannot matter, returns
+// identical bits.
+//
+// Skipping rule.  For a sphere inside box B (centre C, half-diagonal R), a
+// float distance t* puts the point o + t*.d within m = ALPHA * (|o - C| + R)
+// + BETA of B: the float formula's root differs from the geometric one by at
+// most sqrt(|det error|) + |b error| <= ~1.1e-3 * |op| (det = b*b - op.op +
+// rad^2 cancels in float; |op| <= |o - C| + R), and a direction of length
+// 1 +- delta moves the formula's roots by <= sqrt(2 delta) * |op| (rays are
+// normalised or built from unit vectors: delta < 1e-6 -> 1.4e-3 * |op|);
+// ALPHA = 1/64 is more than three times the sum.  So a node whose box,
+// grown by m on every side, is not crossed by the ray between 0 and lim
+// (the current nearest distance, or maxt) holds no sphere that could be
+// taken; its spheres are skipped.  The slab test's own rounding (relative
+// 1e-6, approximate reciprocals and square root) is covered by the same
+// slack.
+// Spheres whose radius dwarfs the rest (the ground) are tested first, for
+// every ray, outside the hierarchy.
+struct BvhView {
+    const float4 *node;   // 2 per node: (centre.xyz, link) (half-extent.xyz, ALPHA*R + BETA)
+    const float4 *geo;    // spheres in hierarchy order: centre, rad^2
+    const int *id;        // their reference indices
+    const float4 *ageo;   // "always" spheres (tested first)
+    const int *aid;
+    int nalways, nnodes;
+};
+constexpr float BVH_ALPHA = 1.f / 64.f;
+
+// One ray query through the hierarchy.  Nearest hit (shadow = false): t in
+// = 1e20f, out = nearest distance, returns its index (highest on ties) or
+// -1.  Any hit (shadow = true): t = maxt, returns an occluder index or -1;
+// with COUNT the highest one (IntersectP's early-exit position, for the test
+// counter), without COUNT the traversal stops at the first.
+template <bool COUNT>
+__device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
+{
+    const float maxt = t;
+    int id = -1;
+    bool stop = false;
+    for (int k = 0; k < B.nalways; k++) {
+        const float d = sphere_hit(B.ageo[k], r);
+        const int i = B.aid[k];
+        if (shadow) {
+            if (d != 0.f && d < maxt && i > id) id = i;
+        } else if (d != 0.f && (d < t || (d == t && i > id))) {
+            t = d;
+            id = i;
+        }
+    }
+    if (!COUNT && shadow && id >= 0) stop = true;
+    // Slab test (culling only: its rounding is inside the margin; fused ops
+    // are fine here and nowhere else).  Zero direction components become
+    // +-1e-30 so no 0 * inf appears.
+    const float dx = fabsf(r.d.x) < 1e-30f ? copysignf(1e-30f, r.d.x) : r.d.x;
+    const float dy = fabsf(r.d.y) < 1e-30f ? copysignf(1e-30f, r.d.y) : r.d.y;
+    const float dz = fabsf(r.d.z) < 1e-30f ? copysignf(1e-30f, r.d.z) : r.d.z;
+    const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
+    const float ax = fabsf(ix), ay = fabsf(iy), az = fabsf(iz);
+    int node = stop ? B.nnodes : 0;
+    while (node < B.nnodes) {
+        const float4 a = B.node[2 * node], b = B.node[2 * node + 1];
+        const int link = __float_as_int(a.w);
+        if (link < 0) {                                  // leaf: first | count << 24
+            const int info = ~link;
+            const int f = info & 0xffffff, e = f + (info >> 24);
+            for (int j = f; j < e; j++) {
+                const float d = sphere_hit(B.geo[j], r);
+                const int i = B.id[j];
+                if (shadow) {
+                    if (d != 0.f && d < maxt && i > id) id = i;
+                } else if (d != 0.f && (d < t || (d == t && i > id))) {
+                    t = d;
+                    id = i;
+                }
+            }
+            node = (!COUNT && shadow && id >= 0) ? B.nnodes : node + 1;   // a leaf's escape is the next node
+        } else {                                         // inner node: link = escape
+            const float lim = shadow ? maxt : t;
+            const float cx = a.x - r.o.x, cy = a.y - r.o.y, cz = a.z - r.o.z;
+            const float dist = __builtin_amdgcn_sqrtf(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, cz * cz)));
+            const float m = __builtin_fmaf(BVH_ALPHA, dist, b.w);
+            const float tcx = cx * ix, tcy = cy * iy, tcz = cz * iz;                // slab centres
+            const float hx = (b.x + m) * ax, hy = (b.y + m) * ay, hz = (b.z + m) * az;  // slab half-widths
+            const float tn = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
+            const float tf = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
+            const bool cross = tn <= tf && tf >= 0.f && tn <= lim;
+            node = cross ? node + 1 : link;
+        }
+    }
+    return id;
+}
+
 struct Counts { unsigned long long isect, isectp, tests, samples; };
 
 // toInt, vec.h:62 (clamp macro keeps -0.0; glibc powf via rt_glibc_math.h).
@@ -121,7 +220,9 @@ __device__ __forceinline__ int to_int(float x)
 #ifndef RT_SPT_MINWAVES
 #define RT_SPT_MINWAVES 1   // __launch_bounds__ min waves per SIMD (occupancy A/B builds)
 #endif
-template <bool DL, bool COUNT, bool LDS>
+constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2;
+
+template <bool DL, bool COUNT, int GEO>
 __global__ void __launch_bounds__(256, RT_SPT_MINWAVES)
 render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,
@@ -129,8 +230,9 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
               int row_begin, int row_end, int first_sample, int nsamples,
               const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
               const float4 *__restrict__ g_col, const int *__restrict__ g_lights, int g_nlights,
-              unsigned long long *__restrict__ counters)
+              BvhView bvh, unsigned long long *__restrict__ counters)
 {
+    constexpr bool LDS = GEO == GEO_LDS;
     // Dynamic LDS carve (16-B aligned base, 16-B multiples): geo | emi | col | lights | count
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Scene S;
@@ -217,7 +319,13 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         while (k < nsamples) {
             float t = shadow ? lmax : 1e20f;
             int first = -1;
-            const int id = query<COUNT>(geo, ray, t, first);
+            int id;
+            if constexpr (GEO == GEO_BVH) {
+                id = query_bvh<COUNT>(bvh, ray, shadow, t);
+                first = id;                 // any hit: the highest occluder (COUNT)
+            } else {
+                id = query<COUNT>(geo, ray, t, first);
+            }
             bool done = false, lights = false;
             if (shadow) {                                       // :154-161
                 cnt.isectp++;
@@ -413,8 +521,10 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
 }  // namespace rt
 
 // ------------------------------------------------------------------ host side
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <vector>
 #include "rt_runtime.h"
 
@@ -426,16 +536,19 @@ struct spt_scene {
     rt_sphere *d_spheres = nullptr;   // n x 44 B
     float4 *d_soa = nullptr;          // geo | emi | col (n each), then lights (int)
     int nlights = 0;
+    void *d_bvh = nullptr;            // nodes | geo | id | always geo | always id (large scenes)
+    rt::smallpt::BvhView bvh = {};
     std::vector<rt_sphere> host;
 };
 
 namespace {
 
-template <bool DL, bool COUNT, bool LDS>
+template <bool DL, bool COUNT, int GEO>
 void launch(dim3 grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam, float *colors,
             const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h, int r0, int r1,
             int first, int ns, unsigned long long *cnt)
 {
+    constexpr bool LDS = GEO == rt::smallpt::GEO_LDS;
     const int n = sc.n;
     const float4 *gg = nullptr, *ge = nullptr, *gc = nullptr;
     const int *gl = nullptr;
@@ -444,23 +557,142 @@ void launch(dim3 grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam,
         gl = (const int *)(gc + n);
     }
     const size_t lds = LDS ? (size_t)n * 3 * sizeof(float4) + (size_t)(n + 1) * sizeof(int) : 0;
-    hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, LDS>), grid, dim3(256), lds, s,
+    hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO>), grid, dim3(256), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, gg, ge,
-                       gc, gl, sc.nlights, cnt);
+                       gc, gl, sc.nlights, sc.bvh, cnt);
 }
 
-template <bool LDS>
+template <int GEO>
 void launch_mode(bool dl, bool count, dim3 grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam,
                  float *colors, const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h,
                  int r0, int r1, int first, int ns, unsigned long long *cnt)
 {
     if (dl) {
-        if (count) launch<true, true, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
-        else launch<true, false, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+        if (count) launch<true, true, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+        else launch<true, false, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
     } else {
-        if (count) launch<false, true, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
-        else launch<false, false, LDS>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+        if (count) launch<false, true, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+        else launch<false, false, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
     }
+}
+
+// ---- hierarchy build (host) for scenes of >= BVH_MIN spheres
+constexpr int BVH_MIN = 256, BVH_LEAF = 4, BVH_MAX_ALWAYS = 16;
+
+struct HostNode { float lo[3], hi[3]; int link; float margin; };
+
+struct BvhBuild {
+    const rt_sphere *sp;
+    std::vector<int> idx;
+    std::vector<HostNode> nodes;
+
+    void box(int i, float *lo, float *hi) const
+    {
+        const rt_sphere &q = sp[i];
+        const float c[3] = {q.p.x, q.p.y, q.p.z};
+        for (int k = 0; k < 3; k++) { lo[k] = c[k] - q.rad; hi[k] = c[k] + q.rad; }
+    }
+    float centre(int i, int k) const { return k == 0 ? sp[i].p.x : (k == 1 ? sp[i].p.y : sp[i].p.z); }
+
+    int build(int lo, int hi)
+    {
+        const int me = (int)nodes.size();
+        nodes.emplace_back();
+        HostNode nd;
+        float clo[3] = {1e30f, 1e30f, 1e30f}, chi[3] = {-1e30f, -1e30f, -1e30f};
+        for (int k = 0; k < 3; k++) { nd.lo[k] = 1e30f; nd.hi[k] = -1e30f; }
+        for (int j = lo; j < hi; j++) {
+            float a[3], b[3];
+            box(idx[j], a, b);
+            for (int k = 0; k < 3; k++) {
+                nd.lo[k] = std::min(nd.lo[k], a[k]);
+                nd.hi[k] = std::max(nd.hi[k], b[k]);
+                clo[k] = std::min(clo[k], centre(idx[j], k));
+                chi[k] = std::max(chi[k], centre(idx[j], k));
+            }
+        }
+        // Margin term ALPHA * diag + BETA; BETA also covers the float rounding
+        // of the box corners (relative 2^-24) and absolute tiny scales.
+        double d2 = 0, mag = 0;
+        for (int k = 0; k < 3; k++) {
+            d2 += (double)(nd.hi[k] - nd.lo[k]) * (nd.hi[k] - nd.lo[k]);
+            mag = std::max(mag, (double)std::max(fabsf(nd.lo[k]), fabsf(nd.hi[k])));
+        }
+        nd.margin = (float)(rt::smallpt::BVH_ALPHA * 0.5 * sqrt(d2) + 1e-3 + 1e-5 * mag);
+        if (hi - lo <= BVH_LEAF) {
+            nd.link = ~(lo | ((hi - lo) << 24));
+        } else {
+            int ax = 0;
+            for (int k = 1; k < 3; k++)
+                if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
+            const int mid = (lo + hi) / 2;
+            std::nth_element(idx.begin() + lo, idx.begin() + mid, idx.begin() + hi, [&](int a, int b) {
+                const float ca = centre(a, ax), cb = centre(b, ax);
+                return ca < cb || (ca == cb && a < b);
+            });
+            build(lo, mid);
+            build(mid, hi);
+            nd.link = (int)nodes.size();                    // escape: first node after this subtree
+        }
+        nodes[me] = nd;
+        return me;
+    }
+};
+
+// Builds the hierarchy into sc->d_bvh / sc->bvh (nothing for small scenes).
+int build_scene_bvh(spt_scene *sc, const rt_sphere *spheres)
+{
+    const int n = sc->n;
+    if (n < BVH_MIN || getenv("RT_SPT_NO_BVH")) return RT_OK;
+    std::vector<float> rads(n);
+    for (int i = 0; i < n; i++) rads[i] = spheres[i].rad;
+    std::nth_element(rads.begin(), rads.begin() + n / 2, rads.end());
+    const float med = rads[n / 2];
+    std::vector<int> always, rest;
+    for (int i = 0; i < n; i++) {
+        if (spheres[i].rad > 64.f * med && (int)always.size() < BVH_MAX_ALWAYS) always.push_back(i);
+        else rest.push_back(i);
+    }
+    BvhBuild b;
+    b.sp = spheres;
+    b.idx = rest;
+    if (!rest.empty()) b.build(0, (int)rest.size());
+    const int nn = (int)b.nodes.size(), nb = (int)rest.size(), na = (int)always.size();
+    std::vector<float4> nodes(2 * (size_t)nn), geo(nb + na);
+    std::vector<int> ids(nb + na);
+    for (int k = 0; k < nn; k++) {
+        const HostNode &h = b.nodes[k];
+        float link;
+        memcpy(&link, &h.link, 4);
+        // centre / half-extent, rounded outward by the BETA slack in h.margin
+        nodes[2 * k] = make_float4(0.5f * (h.lo[0] + h.hi[0]), 0.5f * (h.lo[1] + h.hi[1]), 0.5f * (h.lo[2] + h.hi[2]),
+                                   link);
+        nodes[2 * k + 1] = make_float4(0.5f * (h.hi[0] - h.lo[0]), 0.5f * (h.hi[1] - h.lo[1]),
+                                       0.5f * (h.hi[2] - h.lo[2]), h.margin);
+    }
+    for (int j = 0; j < nb + na; j++) {
+        const int i = j < nb ? b.idx[j] : always[j - nb];
+        const rt_sphere &q = spheres[i];
+        geo[j] = make_float4(q.p.x, q.p.y, q.p.z, q.rad * q.rad);     // geomfunc.h:42 product
+        ids[j] = i;
+    }
+    const size_t nb_bytes = sizeof(float4) * nodes.size(), g_bytes = sizeof(float4) * geo.size(),
+                 i_bytes = sizeof(int) * ids.size();
+    hipError_t e = hipMalloc(&sc->d_bvh, nb_bytes + g_bytes + i_bytes + 16);
+    char *base = (char *)sc->d_bvh;
+    if (e == hipSuccess) e = hipMemcpy(base, nodes.data(), nb_bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(base + nb_bytes, geo.data(), g_bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(base + nb_bytes + g_bytes, ids.data(), i_bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "spt_scene_create hierarchy upload");
+    rt::smallpt::BvhView &v = sc->bvh;
+    v.node = (const float4 *)base;
+    v.geo = (const float4 *)(base + nb_bytes);
+    v.id = (const int *)(base + nb_bytes + g_bytes);
+    v.ageo = v.geo + nb;
+    v.aid = v.id + nb;
+    v.nalways = na;
+    v.nnodes = nn;
+    return RT_OK;
 }
 
 int check_render_args(const rt_camera *camera, float *d_colors, const uint32_t *d_seeds_in,
@@ -514,6 +746,10 @@ extern "C" int spt_scene_create(const rt_sphere *spheres, unsigned nspheres, spt
         delete sc;
         return rtrt::fail_hip(e, "spt_scene_create upload");
     }
+    if ((rc = build_scene_bvh(sc, spheres))) {
+        spt_scene_destroy(sc);
+        return rc;
+    }
     *out = sc;
     return RT_OK;
 }
@@ -525,6 +761,7 @@ extern "C" int spt_scene_destroy(spt_scene *sc)
     (void)hipDeviceSynchronize();
     if (sc->d_spheres) (void)hipFree(sc->d_spheres);
     if (sc->d_soa) (void)hipFree(sc->d_soa);
+    if (sc->d_bvh) (void)hipFree(sc->d_bvh);
     delete sc;
     return RT_OK;
 }
@@ -543,11 +780,15 @@ extern "C" int spt_scene_render_async(const spt_scene *sc, const rt_camera *came
     hipStream_t s = (hipStream_t)stream;
     unsigned long long *cnt = (unsigned long long *)d_counters;
     const bool dl = mode == SPT_DIRECT_LIGHTING;
-    if (sc->n <= rt::smallpt::MAXS_LDS)
-        launch_mode<true>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
+    if (sc->bvh.node)
+        launch_mode<rt::smallpt::GEO_BVH>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in,
+                                          d_seeds_out, d_pixels, w, h, row_begin, row_end, first_sample,
+                                          nsamples, cnt);
+    else if (sc->n <= rt::smallpt::MAXS_LDS)
+        launch_mode<rt::smallpt::GEO_LDS>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
                              d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
     else
-        launch_mode<false>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
+        launch_mode<rt::smallpt::GEO_GLOBAL>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
                               d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
     return rtrt::check_launch("spt render_kernel");
 }

@@ -143,3 +143,52 @@ def test_async_device_paths(rt, oracle):
     for col, seeds, px in outs:
         assert (col.view(np.uint32) == ref[0].view(np.uint32)).all()
         assert (seeds == ref[1]).all() and (px == ref[2]).all()
+
+
+def _bvh_vs_scan(rt, monkeypatch, spheres, n, cam, w, h, spp, mode=0):
+    """Renders with the hierarchy and with the full scan (RT_SPT_NO_BVH):
+    colours, seeds, pixels and counters must be identical bit for bit."""
+    outs = []
+    for no_bvh in (False, True):
+        if no_bvh:
+            monkeypatch.setenv("RT_SPT_NO_BVH", "1")
+        else:
+            monkeypatch.delenv("RT_SPT_NO_BVH", raising=False)
+        f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n, camera=cam, mode=mode)
+        f.render(spp)
+        outs.append(f)
+    a, b = outs
+    assert np.array_equal(a.colors.view(np.uint32), b.colors.view(np.uint32))
+    assert np.array_equal(a.seeds, b.seeds) and np.array_equal(a.pixels, b.pixels)
+    assert a.counters == b.counters
+
+
+def test_bvh_equals_full_scan_configs4(rt, monkeypatch):
+    """configs[4] (10k spheres) at 1920x1080, 2 spp: hierarchy == full scan."""
+    spheres, n, cam = rt.scenes.complex10k()
+    rt.scenes.update_camera(cam, 1920, 1080)
+    _bvh_vs_scan(rt, monkeypatch, spheres, n, cam, 1920, 1080, 2)
+
+
+@pytest.mark.parametrize("seed,mode", [(1, 0), (2, 0), (3, 1), (4, 0)])
+def test_bvh_equals_full_scan_random_scenes(rt, monkeypatch, seed, mode):
+    """Random clouds of small spheres (some overlapping, some tiny, some far),
+    a huge ground sphere and lights, camera inside the cloud: grazing and
+    inside-sphere rays included."""
+    rng = np.random.default_rng(seed)
+    n = 3000
+    S = (rt.Sphere * n)()
+    DIFF, SPEC, REFR = 0, 1, 2
+    rt.scenes._sphere(S[0], 1e4, (0.0, -1e4 - 20.0, 0.0), (0, 0, 0), (0.7, 0.7, 0.7), DIFF)
+    rt.scenes._sphere(S[1], 3.0, (0.0, 40.0, 0.0), (20, 20, 20), (0, 0, 0), DIFF)
+    rt.scenes._sphere(S[2], 0.5, (10.0, 5.0, -5.0), (5, 3, 3), (0, 0, 0), DIFF)
+    for i in range(3, n):
+        scale = 10.0 ** rng.uniform(-2.5, 0.5)
+        c = rng.uniform(-30, 30, 3)
+        refl = int(rng.choice([DIFF, DIFF, DIFF, SPEC, REFR]))
+        rt.scenes._sphere(S[i], scale, tuple(c), (0, 0, 0), tuple(rng.uniform(0.2, 0.9, 3)), refl)
+    cam = rt.Camera()
+    cam.orig = rt.Vec3(1.0, 2.0, 25.0)
+    cam.target = rt.Vec3(0.0, 0.0, 0.0)
+    rt.scenes.update_camera(cam, 160, 120)
+    _bvh_vs_scan(rt, monkeypatch, S, n, cam, 160, 120, 4, mode)
