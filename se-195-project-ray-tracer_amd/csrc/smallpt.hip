@@ -135,7 +135,7 @@ __device__ __forceinline__ int query(const G &geo, const ray3 &r, float &t, int 
 // Spheres whose radius dwarfs the rest (the ground) are tested first, for
 // every ray, outside the hierarchy.
 struct BvhView {
-    const float4 *node;   // 2 per node: (centre.xyz, link) (half-extent.xyz, ALPHA*R + BETA)
+    const float4 *node;   // 8 octant layouts x 2 per node: (centre.xyz, link) (half-extent.xyz, ALPHA*R + BETA)
     const float4 *geo;    // spheres in hierarchy order: centre, rad^2
     const int *id;        // their reference indices
     const float4 *ageo;   // "always" spheres (tested first)
@@ -174,9 +174,12 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
     const float dz = fabsf(r.d.z) < 1e-30f ? copysignf(1e-30f, r.d.z) : r.d.z;
     const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
     const float ax = fabsf(ix), ay = fabsf(iy), az = fabsf(iz);
+    // Layout of this ray's direction octant: near children first.
+    const float4 *nodes = B.node + 2 * (size_t)B.nnodes *
+                                       ((dx < 0.f ? 1 : 0) | (dy < 0.f ? 2 : 0) | (dz < 0.f ? 4 : 0));
     int node = stop ? B.nnodes : 0;
     while (node < B.nnodes) {
-        const float4 a = B.node[2 * node], b = B.node[2 * node + 1];
+        const float4 a = nodes[2 * node], b = nodes[2 * node + 1];
         const int link = __float_as_int(a.w);
         if (link < 0) {                                  // leaf: first | count << 24
             const int info = ~link;
@@ -579,8 +582,15 @@ void launch_mode(bool dl, bool count, dim3 grid, hipStream_t s, const spt_scene 
 // ---- hierarchy build (host) for scenes of >= BVH_MIN spheres
 constexpr int BVH_MIN = 256, BVH_LEAF = 4, BVH_MAX_ALWAYS = 16;
 
-struct HostNode { float lo[3], hi[3]; int link; float margin; };
+struct HostNode {
+    float lo[3], hi[3];
+    int left = -1, right = -1;   // children (inner) ...
+    int first = 0, count = 0;    // ... or the leaf's sphere range
+    int axis = 0;                // split axis (inner)
+    float margin = 0.f;
+};
 
+// Binned-SAH binary tree over sphere boxes (host, once per scene).
 struct BvhBuild {
     const rt_sphere *sp;
     std::vector<int> idx;
@@ -593,6 +603,11 @@ struct BvhBuild {
         for (int k = 0; k < 3; k++) { lo[k] = c[k] - q.rad; hi[k] = c[k] + q.rad; }
     }
     float centre(int i, int k) const { return k == 0 ? sp[i].p.x : (k == 1 ? sp[i].p.y : sp[i].p.z); }
+    static float area(const float *lo, const float *hi)
+    {
+        const float x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+        return x * y + y * z + z * x;
+    }
 
     int build(int lo, int hi)
     {
@@ -611,31 +626,107 @@ struct BvhBuild {
                 chi[k] = std::max(chi[k], centre(idx[j], k));
             }
         }
-        // Margin term ALPHA * diag + BETA; BETA also covers the float rounding
-        // of the box corners (relative 2^-24) and absolute tiny scales.
+        // Margin term ALPHA * R + BETA (R = half diagonal); BETA also covers
+        // the float rounding of the box corners and tiny absolute scales.
         double d2 = 0, mag = 0;
         for (int k = 0; k < 3; k++) {
             d2 += (double)(nd.hi[k] - nd.lo[k]) * (nd.hi[k] - nd.lo[k]);
             mag = std::max(mag, (double)std::max(fabsf(nd.lo[k]), fabsf(nd.hi[k])));
         }
         nd.margin = (float)(rt::smallpt::BVH_ALPHA * 0.5 * sqrt(d2) + 1e-3 + 1e-5 * mag);
-        if (hi - lo <= BVH_LEAF) {
-            nd.link = ~(lo | ((hi - lo) << 24));
-        } else {
-            int ax = 0;
-            for (int k = 1; k < 3; k++)
-                if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
-            const int mid = (lo + hi) / 2;
-            std::nth_element(idx.begin() + lo, idx.begin() + mid, idx.begin() + hi, [&](int a, int b) {
-                const float ca = centre(a, ax), cb = centre(b, ax);
-                return ca < cb || (ca == cb && a < b);
-            });
-            build(lo, mid);
-            build(mid, hi);
-            nd.link = (int)nodes.size();                    // escape: first node after this subtree
+        const int n = hi - lo;
+        if (n <= BVH_LEAF) {
+            nd.first = lo;
+            nd.count = n;
+            nodes[me] = nd;
+            return me;
         }
+        // SAH over 16 centroid bins per axis.
+        constexpr int NB = 16;
+        int best_ax = -1, best_b = 0;
+        float best_cost = 1e30f;
+        for (int ax = 0; ax < 3; ax++) {
+            const float ext = chi[ax] - clo[ax];
+            if (!(ext > 0.f)) continue;
+            int cnt[NB] = {};
+            float blo[NB][3], bhi[NB][3];
+            for (int q = 0; q < NB; q++)
+                for (int k = 0; k < 3; k++) { blo[q][k] = 1e30f; bhi[q][k] = -1e30f; }
+            for (int j = lo; j < hi; j++) {
+                int q = (int)((centre(idx[j], ax) - clo[ax]) / ext * NB);
+                q = std::min(std::max(q, 0), NB - 1);
+                float a[3], b[3];
+                box(idx[j], a, b);
+                cnt[q]++;
+                for (int k = 0; k < 3; k++) { blo[q][k] = std::min(blo[q][k], a[k]); bhi[q][k] = std::max(bhi[q][k], b[k]); }
+            }
+            float rlo[NB][3], rhi[NB][3];
+            int rc[NB];
+            float alo[3] = {1e30f, 1e30f, 1e30f}, ahi[3] = {-1e30f, -1e30f, -1e30f};
+            int ac = 0;
+            for (int q = NB - 1; q >= 1; q--) {
+                for (int k = 0; k < 3; k++) { alo[k] = std::min(alo[k], blo[q][k]); ahi[k] = std::max(ahi[k], bhi[q][k]); }
+                ac += cnt[q];
+                for (int k = 0; k < 3; k++) { rlo[q][k] = alo[k]; rhi[q][k] = ahi[k]; }
+                rc[q] = ac;
+            }
+            float llo[3] = {1e30f, 1e30f, 1e30f}, lhi[3] = {-1e30f, -1e30f, -1e30f};
+            int lc = 0;
+            for (int q = 0; q < NB - 1; q++) {
+                for (int k = 0; k < 3; k++) { llo[k] = std::min(llo[k], blo[q][k]); lhi[k] = std::max(lhi[k], bhi[q][k]); }
+                lc += cnt[q];
+                if (lc == 0 || rc[q + 1] == 0) continue;
+                const float cost = area(llo, lhi) * lc + area(rlo[q + 1], rhi[q + 1]) * rc[q + 1];
+                if (cost < best_cost) { best_cost = cost; best_ax = ax; best_b = q + 1; }
+            }
+        }
+        int mid;
+        if (best_ax >= 0) {
+            const int ax = best_ax;
+            const float ext = chi[ax] - clo[ax];
+            auto it = std::partition(idx.begin() + lo, idx.begin() + hi, [&](int i) {
+                int q = (int)((centre(i, ax) - clo[ax]) / ext * NB);
+                q = std::min(std::max(q, 0), NB - 1);
+                return q < best_b;
+            });
+            mid = (int)(it - idx.begin());
+            nd.axis = ax;
+        } else {
+            mid = lo + n / 2;   // all centres equal: any split
+        }
+        if (mid == lo || mid == hi) mid = lo + n / 2;
+        nd.left = build(lo, mid);
+        nd.right = build(mid, hi);
         nodes[me] = nd;
         return me;
+    }
+
+    // Depth-first layout for ray-direction octant `oct` (bit k set: d_k < 0):
+    // at each inner node the child on the near side of its split axis comes
+    // first; link = escape index (inner) or ~(first | count << 24) (leaf).
+    void emit(int node, int oct, std::vector<float4> &out) const
+    {
+        const HostNode &h = nodes[node];
+        const size_t me = out.size() / 2;
+        out.push_back(make_float4(0.5f * (h.lo[0] + h.hi[0]), 0.5f * (h.lo[1] + h.hi[1]), 0.5f * (h.lo[2] + h.hi[2]),
+                                  0.f));
+        out.push_back(make_float4(0.5f * (h.hi[0] - h.lo[0]), 0.5f * (h.hi[1] - h.lo[1]), 0.5f * (h.hi[2] - h.lo[2]),
+                                  h.margin));
+        int link;
+        if (h.left < 0) {
+            link = ~(h.first | (h.count << 24));
+        } else {
+            const HostNode &L = nodes[h.left], &R = nodes[h.right];
+            const bool l_low = L.lo[h.axis] + L.hi[h.axis] <= R.lo[h.axis] + R.hi[h.axis];
+            const bool neg = (oct >> h.axis) & 1;
+            const int c0 = (l_low != neg) ? h.left : h.right;
+            emit(c0, oct, out);
+            emit(c0 == h.left ? h.right : h.left, oct, out);
+            link = (int)(out.size() / 2);                   // escape: the node after this subtree
+        }
+        float f;
+        memcpy(&f, &link, 4);
+        out[2 * me].w = f;
     }
 };
 
@@ -658,18 +749,17 @@ int build_scene_bvh(spt_scene *sc, const rt_sphere *spheres)
     b.idx = rest;
     if (!rest.empty()) b.build(0, (int)rest.size());
     const int nn = (int)b.nodes.size(), nb = (int)rest.size(), na = (int)always.size();
-    std::vector<float4> nodes(2 * (size_t)nn), geo(nb + na);
-    std::vector<int> ids(nb + na);
-    for (int k = 0; k < nn; k++) {
-        const HostNode &h = b.nodes[k];
-        float link;
-        memcpy(&link, &h.link, 4);
-        // centre / half-extent, rounded outward by the BETA slack in h.margin
-        nodes[2 * k] = make_float4(0.5f * (h.lo[0] + h.hi[0]), 0.5f * (h.lo[1] + h.hi[1]), 0.5f * (h.lo[2] + h.hi[2]),
-                                   link);
-        nodes[2 * k + 1] = make_float4(0.5f * (h.hi[0] - h.lo[0]), 0.5f * (h.hi[1] - h.lo[1]),
-                                       0.5f * (h.hi[2] - h.lo[2]), h.margin);
+    // Eight layouts (one per direction octant), each with layout-local links.
+    std::vector<float4> nodes;
+    nodes.reserve(2 * (size_t)nn * 8);
+    for (int oct = 0; oct < 8; oct++) {
+        std::vector<float4> lay;
+        lay.reserve(2 * (size_t)nn);
+        if (nn) b.emit(0, oct, lay);
+        nodes.insert(nodes.end(), lay.begin(), lay.end());
     }
+    std::vector<float4> geo(nb + na);
+    std::vector<int> ids(nb + na);
     for (int j = 0; j < nb + na; j++) {
         const int i = j < nb ? b.idx[j] : always[j - nb];
         const rt_sphere &q = spheres[i];
