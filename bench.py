@@ -139,6 +139,60 @@ def whitted_line(args, dev):
     return out
 
 
+def c5_line(args, dev):
+    """Side line: BASELINE configs[4], the 10k-sphere scene_build_complex scene
+    at 1920x1080, 64 spp, one frame on 1 GPU (the exact-culling hierarchy
+    path), HIP events; CPU baseline on a band of rows at 1 spp."""
+    spheres, n, cam = rtamd.scenes.complex10k()
+    rtamd.scenes.update_camera(cam, W, H)
+    sc = rtamd.SmallptScene(spheres, n)
+    seeds0 = torch.from_numpy(rtamd.scenes.seeds(W, H).view(np.int32)).to(dev)
+    seeds = torch.empty_like(seeds0)
+    col = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
+    px = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev)
+    L = rtamd.lib()
+
+    def run(c):
+        rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                             seeds.data_ptr(), px.data_ptr(), W, H, 0, H, 0, SPP,
+                                             rtamd.SPT_PATH_TRACING, c.data_ptr() if c is not None else None,
+                                             s.cuda_stream))
+
+    run(cnt)
+    torch.cuda.synchronize(dev)
+    counts = cnt.tolist()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    run(None)
+    e1.record(s)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1)
+    rays = counts[0] + counts[1]
+    out = {"workload": "configs[4]: scene_build_complex 10k spheres, 1920x1080, 64 spp, one frame",
+           "ms_per_frame": round(ms, 3), "Mrays_per_s": round(rays / ms / 1e3, 2), "rays_per_frame": rays,
+           "sphere_tests_reference": counts[2]}
+    if not args.no_cpu:
+        import oracle_lib as O
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        ccol = np.zeros(3 * W * H, np.float32)
+        cpx = np.zeros(W * H, np.uint32)
+        rows, dt = 8, 0.0
+        for _ in range(2):                 # probe, then a band sized to ~3 s
+            if dt:
+                rows = int(min(H, max(rows, rows * 3.0 / max(dt, 1e-3))))
+            r0 = H // 2 - rows // 2
+            t0 = time.perf_counter()
+            c = O.smallpt_render(spheres, n, cam, ccol, rtamd.scenes.seeds(W, H), cpx, W, H, 0, 1,
+                                 row_begin=r0, row_end=r0 + rows, nthreads=threads)
+            dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round((c[0] + c[1]) / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads,
+                               "kind": "port", "sample": "oracle/smallpt_oracle.c (full scan), rows [%d,%d) at 1 spp, "
+                               "%.1f s" % (r0, r0 + rows, dt)}
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -258,6 +312,7 @@ def main():
     if rank == 0 and world == 1:
         if not args.no_whitted:
             out["whitted"] = whitted_line(args, dev)
+            out["configs4"] = c5_line(args, dev)
         out["cpu_baseline"] = None if args.no_cpu else cpu_baseline(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
