@@ -56,19 +56,22 @@ __device__ __forceinline__ v3 vxcross(v3 a, v3 b)
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 
-// SphereIntersect, geomfunc.h:32-59 (g = centre.xyz, rad*rad).  The early
-// return on det < 0 is kept as a branch: when no lane of the wave reaches the
-// sphere's line the square root is skipped (measured +8 % over a branch-free
-// select form).  NaN det yields 0, as in the reference.
+// SphereIntersect, geomfunc.h:32-59 (g = centre.xyz, rad*rad), except that a
+// miss returns +inf instead of 0: every caller tests "d != 0 && d < t" with a
+// finite t, which for +inf is the single test "d < t".  The early return on
+// det < 0 is kept as a branch: when no lane of the wave reaches the sphere's
+// line the square root is skipped (measured +8 % over a branch-free select
+// form).  NaN det is a miss, as in the reference.
+constexpr float MISS = __builtin_inff();
 __device__ __forceinline__ float sphere_hit(float4 g, const ray3 &r)
 {
     const float opx = g.x - r.o.x, opy = g.y - r.o.y, opz = g.z - r.o.z;
     const float b = opx * r.d.x + opy * r.d.y + opz * r.d.z;
     const float det = b * b - (opx * opx + opy * opy + opz * opz) + g.w;
-    if (det < 0.f) return 0.f;
+    if (det < 0.f) return MISS;
     const float sd = sqrt_exact(det);
     const float t1 = b - sd, t2 = b + sd;
-    return t1 > EPS ? t1 : (t2 > EPS ? t2 : 0.f);
+    return t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
 }
 
 // Sphere geometry for the nearest-hit / any-hit loops: LDS (per-block copy)
@@ -101,7 +104,7 @@ __device__ __forceinline__ int query(const G &geo, const ray3 &r, float &t, int 
 #pragma unroll 1
     for (int i = geo.count() - 1; i >= 0; i--) {
         const float d = sphere_hit(geo.at(i), r);
-        const bool take = (d != 0.f) && (d < t);
+        const bool take = d < t;                           // d != 0 && d < t (miss = +inf)
         t = take ? d : t;
         id = take ? i : id;
         if (COUNT) first = (first < 0 && take) ? i : first;
@@ -159,8 +162,8 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
         const float d = sphere_hit(B.ageo[k], r);
         const int i = B.aid[k];
         if (shadow) {
-            if (d != 0.f && d < maxt && i > id) id = i;
-        } else if (d != 0.f && (d < t || (d == t && i > id))) {
+            if (d < maxt && i > id) id = i;
+        } else if (d < t || (d == t && i > id)) {
             t = d;
             id = i;
         }
@@ -188,8 +191,8 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
                 const float d = sphere_hit(B.geo[j], r);
                 const int i = B.id[j];
                 if (shadow) {
-                    if (d != 0.f && d < maxt && i > id) id = i;
-                } else if (d != 0.f && (d < t || (d == t && i > id))) {
+                    if (d < maxt && i > id) id = i;
+                } else if (d < t || (d == t && i > id)) {
                     t = d;
                     id = i;
                 }
