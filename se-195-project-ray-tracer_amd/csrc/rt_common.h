@@ -42,9 +42,10 @@ __device__ __forceinline__ float sqrt_rn(float x)
 
 // Short correctly rounded forms on the normal range, each checked against the
 // IEEE result for all 2^32 inputs on the device (tests/test_gpu_math.py):
-//  * sqrt_nr: v_sqrt_f32, then one residual correction s + (x - s*s) / (2s)
-//    with 1/(2s) from v_rsq_f32 -- equal to sqrtf(x) for x in [2^-96, inf)
-//    (differences start below 2^-102);
+//  * sqrt_nr: s = x * v_rsq_f32(x), then one residual correction
+//    s + (x - s*s) * rsq(x) / 2 -- equal to sqrtf(x) for x in [2^-96, inf)
+//    (differences start below 2^-102).  One transcendental: a form with both
+//    v_sqrt_f32 and v_rsq_f32 was measured 7 % slower on the smallpt kernel;
 //  * rcp_nr: v_rcp_f32 and one Newton step -- equal to 1.f / x for
 //    2^-126 <= |x| < 2^126 (outside it the result or input is denormal).
 // Callers guard the domain with a wave-uniform branch to the general
@@ -57,10 +58,10 @@ __device__ __forceinline__ bool sqrt_nr_ok(float x)     // 2^-96 <= x < +inf (no
 
 __device__ __forceinline__ float sqrt_nr(float x)
 {
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float h = 0.5f * __builtin_amdgcn_rsqf(x);
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s = x * y;
     const float r = __builtin_fmaf(-s, s, x);
-    return __builtin_fmaf(r, h, s);
+    return __builtin_fmaf(r, 0.5f * y, s);
 }
 
 __device__ __forceinline__ float rcp_nr(float x)
