@@ -201,13 +201,20 @@ def main():
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     distributed = world > 1
+    # Rehearsal knobs for a one-GPU box (never set by the driver):
+    # RT_BENCH_BACKEND=gloo and RT_BENCH_SHARE_GPU=1 run N ranks on device 0.
+    backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
+    gpu = local % torch.cuda.device_count() if os.environ.get("RT_BENCH_SHARE_GPU") else local
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
-    rtamd.set_device(local)
+    rtamd.set_device(gpu)
     L = rtamd.lib()
 
     spheres, ns = rtamd.scenes.cornell()
