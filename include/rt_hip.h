@@ -88,6 +88,21 @@ int rtw_render(const rt_primitive *prims, int nprims, uint32_t *xrgb, int w, int
 int rtw_render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int w, int h,
                      int row_begin, int row_end, uint64_t *d_counters, void *stream);
 
+/* The reference's own device kernel instead of its CPU path: raytrace_kernel
+ * of raytracer3.0.06.no_rec.samp/openCLcode.cl:5-247 with openCLcode.h's
+ * Engine_Raytrace (ExecuteKernel, openCLcode.cpp:537-560) -- rows
+ * [20, min(530, h)) (openCLcode.cl:66-67), SX = WX1 + x*DX per pixel (:22-23),
+ * 2x2 sub-samples (:66), a light hit adds the light's colour
+ * (openCLcode.h:176-182), reflection child folded before the refraction child
+ * (:199-233), x(256/4) scale (:238-240).  The OpenCL built-ins (sqrt, '/',
+ * exp, pow) are computed as the CPU path's correctly rounded / glibc
+ * functions.  Same counters as rtw_render.  Rows outside the window are not
+ * written. */
+int rtw_render_ocl(const rt_primitive *prims, int nprims, uint32_t *xrgb, int w, int h,
+                   uint64_t *counters);
+int rtw_render_ocl_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int w, int h,
+                         uint64_t *d_counters, void *stream);
+
 /* ------------------------------------------------------------ smallpt */
 #define SPT_PATH_TRACING 0       /* RadiancePathTracing    geomfunc.h:167-338 */
 #define SPT_DIRECT_LIGHTING 1    /* RadianceDirectLighting geomfunc.h:340-483 */

@@ -70,6 +70,9 @@ int  orw_scene_init(or_primitive *out, int cap);
  * nthreads: 1 = the reference's single thread; >1 = OpenMP over rows. */
 void orw_render(const or_primitive *prims, int n, uint32_t *dest, int w, int h,
                 int row_begin, int row_end, uint64_t *counters, int nthreads);
+/* GPU-semantics variant: raytrace_kernel of openCLcode.cl (rows [20, min(530,h))). */
+void orw_render_ocl(const or_primitive *prims, int n, uint32_t *dest, int w, int h,
+                    uint64_t *counters, int nthreads);
 
 /* Single primitive helpers, exposed for unit tests (scene.cpp:34-53,125-190). */
 int  orw_primitive_intersect(const or_primitive *p, const float ray[6], float *dist);

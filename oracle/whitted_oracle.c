@@ -143,10 +143,12 @@ void orw_primitive_normal(const or_primitive *p, const float pos[3], float out[3
 typedef struct { uint64_t traced, shadow, tests, tir; } wcount;
 
 /* Engine_Raytrace, raytracer.cpp:30-271 */
+/* ocl != 0: the device twin in openCLcode.h:150-390, identical except that a
+ * light hit adds the light's colour (openCLcode.h:176-182) instead of 1. */
 static int engine_raytrace(const or_primitive *P, int n, const ray_t *a_ray, vec3 *acc,
                            int depth, float *a_rindex, float *a_dist, float *a_refl,
                            int *a_refl_index, ray_t *a_refl_ray, float *a_refr,
-                           int *a_refr_index, ray_t *a_refr_ray, wcount *cnt)
+                           int *a_refr_index, ray_t *a_refr_ray, wcount *cnt, int ocl)
 {
     if (depth > TRACEDEPTH) return -1;
     cnt->traced++;
@@ -160,7 +162,8 @@ static int engine_raytrace(const or_primitive *P, int n, const ray_t *a_ray, vec
     if (hit_once == 0) return -1;                                   /* :51 */
     const or_primitive *pr = &P[prim_index];
     if (pr->m_Light > 0) {                                          /* :53-57 */
-        acc->x += 1; acc->y += 1; acc->z += 1;
+        if (ocl) { acc->x += pr->m_Color.x; acc->y += pr->m_Color.y; acc->z += pr->m_Color.z; }
+        else { acc->x += 1; acc->y += 1; acc->z += 1; }
         return prim_index;
     }
     vec3 pi;                                                        /* :61-65 */
@@ -271,8 +274,11 @@ static int engine_raytrace(const or_primitive *P, int n, const ray_t *a_ray, vec
 
 /* One pixel of Engine_Render (raytracer.cpp:311-525): 3x3 sub-samples, the
  * 63-node breadth-first ray tree, back-accumulation and XRGB pack. */
+/* ocl != 0: raytrace_kernel of openCLcode.cl:5-247 -- 2x2 sub-samples
+ * (tx, ty in {-1, 0}, :66), refl child folded before refr child (:199-233),
+ * x(256/4) scale (:238-240); SX/SY come from the caller. */
 static uint32_t render_pixel(const or_primitive *P, int n, float SX, float SY,
-                             float DX, float DY, wcount *cnt)
+                             float DX, float DY, wcount *cnt, int ocl)
 {
     vec3 camera = {0.0f, 0.25f, -7.0f};                             /* :315 */
     vec3 total = {0, 0, 0};
@@ -282,7 +288,8 @@ static uint32_t render_pixel(const or_primitive *P, int n, float SX, float SY,
     float tr_refl[NODECOUNT], tr_refr[NODECOUNT], tr_rindex[NODECOUNT], tr_dist[NODECOUNT];
     int tr_refl_index[NODECOUNT], tr_refr_index[NODECOUNT];
 
-    for (int tx = -1; tx < 2; tx++) for (int ty = -1; ty < 2; ty++) { /* :351 */
+    const int tend = ocl ? 1 : 2;
+    for (int tx = -1; tx < tend; tx++) for (int ty = -1; ty < tend; ty++) { /* :351 */
         for (int i = 0; i < NODECOUNT; i++) {
             cx[i] = cy[i] = cz[i] = 0;
             tr_refl[i] = 0; tr_refl_index[i] = -1; tr_rindex[i] = 1.0f;
@@ -305,7 +312,7 @@ static uint32_t render_pixel(const or_primitive *P, int n, float SX, float SY,
         int refl_index = -1, refr_index = -1;
         vec3 acc = {0, 0, 0};
         engine_raytrace(P, n, &o_ray, &acc, 1, &rin, &dist, &refl, &refl_index, &refl_ray,
-                        &refr, &refr_index, &refr_ray, cnt);        /* :383 */
+                        &refr, &refr_index, &refr_ray, cnt, ocl);   /* :383 */
         cx[0] = acc.x; cy[0] = acc.y; cz[0] = acc.z;
         tr_refl_ray[0] = refl_ray; tr_refl[0] = refl; tr_refl_index[0] = refl_index;
         tr_refr_ray[0] = refr_ray; tr_rindex[0] = rin; tr_refr[0] = refr;
@@ -323,7 +330,7 @@ static uint32_t render_pixel(const or_primitive *P, int n, float SX, float SY,
                     dist = 0; refl = 0; refr = 0; refl_index = -1; refr_index = -1;
                     rin = tr_rindex[p];
                     engine_raytrace(P, n, &o_ray, &acc, 1, &rin, &dist, &refl, &refl_index,
-                                    &refl_ray, &refr, &refr_index, &refr_ray, cnt);
+                                    &refl_ray, &refr, &refr_index, &refr_ray, cnt, ocl);
                     cx[c] = acc.x; cy[c] = acc.y; cz[c] = acc.z;
                     tr_refl_ray[c] = refl_ray; tr_refl[c] = refl; tr_refl_index[c] = refl_index;
                     tr_refr_ray[c] = refr_ray; tr_refr[c] = refr; tr_refr_index[c] = refr_index;
@@ -339,32 +346,40 @@ static uint32_t render_pixel(const or_primitive *P, int n, float SX, float SY,
 
         for (int i = NODECOUNT - 1; i >= 2; i -= 2) {               /* :476-511 */
             int p = (i - 1) / 2;
-            acc.x = cx[i]; acc.y = cy[i]; acc.z = cz[i];
-            if ((tr_refr_index[p] > -1) && (tr_refr[p] > 0)) {
-                const or_primitive *q = &P[tr_refr_index[p]];
-                vec3 ab;
-                ab.x = q->m_Color.x * 0.15f * -tr_dist[p];
-                ab.y = q->m_Color.y * 0.15f * -tr_dist[p];
-                ab.z = q->m_Color.z * 0.15f * -tr_dist[p];
-                acc.x = cx[i] * expf(ab.x);
-                acc.y = cy[i] * expf(ab.y);
-                acc.z = cz[i] * expf(ab.z);
+            for (int k = 0; k < 2; k++) {
+                /* CPU: refraction child (i) then reflection child (i-1);
+                 * openCLcode.cl:199-233: reflection child first. */
+                const int refr_side = ocl ? (k == 1) : (k == 0);
+                if (refr_side) {
+                    acc.x = cx[i]; acc.y = cy[i]; acc.z = cz[i];
+                    if ((tr_refr_index[p] > -1) && (tr_refr[p] > 0)) {
+                        const or_primitive *q = &P[tr_refr_index[p]];
+                        vec3 ab;
+                        ab.x = q->m_Color.x * 0.15f * -tr_dist[p];
+                        ab.y = q->m_Color.y * 0.15f * -tr_dist[p];
+                        ab.z = q->m_Color.z * 0.15f * -tr_dist[p];
+                        acc.x = cx[i] * expf(ab.x);
+                        acc.y = cy[i] * expf(ab.y);
+                        acc.z = cz[i] * expf(ab.z);
+                    }
+                } else {
+                    acc.x = cx[i - 1]; acc.y = cy[i - 1]; acc.z = cz[i - 1];
+                    if ((tr_refl_index[p] > -1) && (tr_refl[p] > 0)) {
+                        const or_primitive *q = &P[tr_refl_index[p]];
+                        acc.x = cx[i - 1] * q->m_Color.x * tr_refl[p];
+                        acc.y = cy[i - 1] * q->m_Color.y * tr_refl[p];
+                        acc.z = cz[i - 1] * q->m_Color.z * tr_refl[p];
+                    }
+                }
+                cx[p] += acc.x; cy[p] += acc.y; cz[p] += acc.z;
             }
-            cx[p] += acc.x; cy[p] += acc.y; cz[p] += acc.z;
-            acc.x = cx[i - 1]; acc.y = cy[i - 1]; acc.z = cz[i - 1];
-            if ((tr_refl_index[p] > -1) && (tr_refl[p] > 0)) {
-                const or_primitive *q = &P[tr_refl_index[p]];
-                acc.x = cx[i - 1] * q->m_Color.x * tr_refl[p];
-                acc.y = cy[i - 1] * q->m_Color.y * tr_refl[p];
-                acc.z = cz[i - 1] * q->m_Color.z * tr_refl[p];
-            }
-            cx[p] += acc.x; cy[p] += acc.y; cz[p] += acc.z;
         }
         total.x += cx[0]; total.y += cy[0]; total.z += cz[0];        /* :513-515 */
     }
-    int red = (int)(total.x * (256 / 9));                          /* :517-523 */
-    int green = (int)(total.y * (256 / 9));
-    int blue = (int)(total.z * (256 / 9));
+    const int scale = ocl ? (256 / 4) : (256 / 9);                  /* openCLcode.cl:238-240 */
+    int red = (int)(total.x * scale);                               /* :517-523 */
+    int green = (int)(total.y * scale);
+    int blue = (int)(total.z * scale);
     if (red > 255) red = 255;
     if (green > 255) green = 255;
     if (blue > 255) blue = 255;
@@ -395,7 +410,38 @@ void orw_render(const or_primitive *P, int n, uint32_t *dest, int w, int h,
     for (int y = row_begin; y < row_end; y++) {
         wcount c = {0, 0, 0, 0};
         for (int x = 0; x < w; x++)
-            dest[(size_t)y * w + x] = render_pixel(P, n, SXcol[x], SYrow[y], DX, DY, &c);
+            dest[(size_t)y * w + x] = render_pixel(P, n, SXcol[x], SYrow[y], DX, DY, &c, 0);
+        t_traced += c.traced; t_shadow += c.shadow; t_tests += c.tests; t_tir += c.tir;
+    }
+    if (counters) {
+        counters[0] = t_traced; counters[1] = t_shadow;
+        counters[2] = t_tests; counters[3] = t_tir;
+    }
+}
+
+/* raytrace_kernel of openCLcode.cl:5-247 on the CPU: rows [20, min(530, h))
+ * (:66-67), SX = WX1 + x*DX and SY = WY1 + y*DY per pixel (:22-23), 2x2
+ * sub-samples, light colour on light hits, refl-before-refr folding, x64.
+ * The OpenCL built-ins (sqrt, '/', exp, pow) are taken as the correctly
+ * rounded / glibc functions of the CPU path. */
+void orw_render_ocl(const or_primitive *P, int n, uint32_t *dest, int w, int h,
+                    uint64_t *counters, int nthreads)
+{
+    const float WX1 = -3.0f, WX2 = 3.0f, WY1 = 2.25f, WY2 = -2.25f;
+    const float DX = (WX2 - WX1) / w;
+    const float DY = (WY2 - WY1) / h;
+    const int row_end = h < 530 ? h : 530;
+    uint64_t t_traced = 0, t_shadow = 0, t_tests = 0, t_tir = 0;
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) \
+    reduction(+ : t_traced, t_shadow, t_tests, t_tir) if (nthreads > 1)
+    for (int y = 20; y < row_end; y++) {
+        wcount c = {0, 0, 0, 0};
+        const float SY = WY1 + y * DY;
+        for (int x = 0; x < w; x++) {
+            const float SX = WX1 + x * DX;
+            dest[(size_t)y * w + x] = render_pixel(P, n, SX, SY, DX, DY, &c, 1);
+        }
         t_traced += c.traced; t_shadow += c.shadow; t_tests += c.tests; t_tir += c.tir;
     }
     if (counters) {

@@ -23,6 +23,7 @@ struct DeviceState {
     // SLOT_VIEW (whitted.hip).
     int vt_w = 0, vt_h = 0;
     float vt_DX = 0.f, vt_DY = 0.f;
+    int vto_w = 0, vto_h = 0;          // openCLcode.cl-semantics tables (whitted.hip)
 };
 
 // Records msg (plus the HIP error string) for rt_last_error(); returns code.

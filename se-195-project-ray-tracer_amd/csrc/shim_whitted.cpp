@@ -10,6 +10,10 @@
 // CPU path's image (Engine_Render, raytracer.cpp:301-530) bit for bit over
 // the rows Engine_Render covers: [m_CurrLine, m_Height - 70).
 //
+// With RT_WHITTED_SEMANTICS=opencl in the environment the shim computes what
+// the reference's own OpenCL kernel computes instead (rtw_render_ocl_async:
+// rows [20, min(530, h)), 2x2 sub-samples, light colour, x64).
+//
 // Error behaviour follows the reference host: print to stderr and exit(-1).
 #include <stdio.h>
 #include <stdlib.h>
@@ -44,6 +48,25 @@ uint32_t *d_dest = nullptr;            // device frame (m_Width * m_Height)
 int dev_w = 0, dev_h = 0, dev_nprims = 0, prim_cap = 0;
 int arg_w = 0, arg_h = 0, arg_nprims = 0, arg_row0 = 20;
 hipStream_t stream = nullptr;
+
+bool opencl_semantics()
+{
+    const char *e = getenv("RT_WHITTED_SEMANTICS");
+    return e && strcmp(e, "opencl") == 0;
+}
+
+// Rows the device writes: Engine_Render's [m_CurrLine, m_Height - 70), or
+// raytrace_kernel's [20, min(530, height)).
+void window(int *r0, int *r1)
+{
+    if (opencl_semantics()) {
+        *r0 = 20;
+        *r1 = arg_h < 530 ? arg_h : 530;
+    } else {
+        *r0 = arg_row0;
+        *r1 = arg_h - 70;
+    }
+}
 
 void die(const char *what, int rc)
 {
@@ -123,9 +146,12 @@ void SetKernelArguments()
 // ExecuteKernel (openCLcode.cpp:537-560): one launch over the render window.
 void ExecuteKernel()
 {
-    const int row1 = arg_h - 70;
-    if (row1 <= arg_row0) return;       // Engine_Render's loop would not run either
-    int rc = rtw_render_async(d_prims, arg_nprims, d_dest, arg_w, arg_h, arg_row0, row1, nullptr, stream);
+    int row0, row1;
+    window(&row0, &row1);
+    if (row1 <= row0) return;           // the reference loop would not run either
+    const int rc = opencl_semantics()
+                       ? rtw_render_ocl_async(d_prims, arg_nprims, d_dest, arg_w, arg_h, nullptr, stream)
+                       : rtw_render_async(d_prims, arg_nprims, d_dest, arg_w, arg_h, row0, row1, nullptr, stream);
     if (rc) die("Failed to enqueue HIP work", rc);
 }
 
@@ -134,10 +160,11 @@ void ExecuteKernel()
 // host's contents (the CPU path never writes them).
 void ReadKernelBuffer()
 {
-    const int row1 = arg_h - 70;
+    int row0, row1;
+    window(&row0, &row1);
     hipError_t e;
-    if (row1 > arg_row0) {
-        const size_t off = (size_t)arg_row0 * arg_w, len = (size_t)(row1 - arg_row0) * arg_w;
+    if (row1 > row0) {
+        const size_t off = (size_t)row0 * arg_w, len = (size_t)(row1 - row0) * arg_w;
         e = hipMemcpyAsync(m_Dest + off, d_dest + off, sizeof(uint32_t) * len, hipMemcpyDeviceToHost, stream);
         if (e != hipSuccess) die_hip("Failed to read the HIP pixel buffer", e);
     }

@@ -124,7 +124,9 @@ struct Counts { unsigned long long traced, shadow, tests, tir; };
 
 // Engine_Raytrace, raytracer.cpp:30-271 (a_Depth is always 1 at every call
 // site, so the TRACEDEPTH guards are constant-true).
-__device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &cnt)
+// ocl: the device twin of openCLcode.h:150-390 -- a light hit adds the
+// light's colour (openCLcode.h:176-182) instead of (1,1,1); all else equal.
+__device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &cnt, bool ocl)
 {
     Hit h;
     h.acc = mk(0.f, 0.f, 0.f);
@@ -155,7 +157,12 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
     if (!hit_once) return h;                            // :51
     h.prim = prim;
     if (S.light[prim] > 0) {                            // :53-57
-        h.acc = mk(1.f, 1.f, 1.f);
+        if (ocl) {
+            const float4 lc = S.mat0[prim];
+            h.acc = mk(lc.x, lc.y, lc.z);
+        } else {
+            h.acc = mk(1.f, 1.f, 1.f);
+        }
         return h;
     }
     v3 pi;                                              // :61-65
@@ -274,9 +281,10 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
 }
 
 // Primary ray of sub-sample `sub` (tx outer, ty inner: raytracer.cpp:351,364-367).
-__device__ __forceinline__ ray3 primary(int sub, float SX, float SY, float DX, float DY)
+// side = 3 (CPU path, tx/ty in -1..1) or 2 (openCLcode.cl:66, tx/ty in -1..0).
+__device__ __forceinline__ ray3 primary(int sub, float SX, float SY, float DX, float DY, int side)
 {
-    const float tx = (float)(sub / 3 - 1), ty = (float)(sub % 3 - 1);
+    const float tx = (float)(sub / side - 1), ty = (float)(sub % side - 1);
     v3 d;
     d.x = (SX + DX * tx / 2.0f) - 0.0f;
     d.y = (SY + DY * ty / 2.0f) - 0.25f;
@@ -402,6 +410,8 @@ struct WfArgs {
     int4 *tir[LEVELS];        // [tcap] TIR nodes of level L: slot, tree, node, rindex (bits)
     int *count;               // [C_TOTAL * CSTRIDE]
     int cap, segcap, tcap, ntrees, npix, w, row_begin;   // cap = NSEG * segcap
+    int side, nsub;           // sub-sample grid: 3 x 3 (CPU path) or 2 x 2 (openCLcode.cl)
+    bool ocl;                 // openCLcode.cl semantics (light colour, refl-first folding, x64)
 };
 
 __device__ void flag_tree(const WfArgs &A, int tree)
@@ -525,11 +535,11 @@ root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float
     const int pix = (y - A.row_begin) * A.w + x;
     const float SX = active ? sx_tab[x] : 0.f, SY = active ? sy_tab[y] : 0.f;
     Counts cnt = {0, 0, 0, 0};
-    for (int sub = 0; sub < 9; sub++) {
+    for (int sub = 0; sub < A.nsub; sub++) {
         Hit hh;
         bool tir = false;
         if (active) {
-            hh = trace(S, primary(sub, SX, SY, DX, DY), 1.0f, cnt);
+            hh = trace(S, primary(sub, SX, SY, DX, DY, A.side), 1.0f, cnt, A.ocl);
             tir = hh.refr > 0 && !hh.refr_ray_ok;
             if (tir) cnt.tir++;
         }
@@ -574,7 +584,7 @@ level_kernel(WfArgs A, int L, unsigned long long *__restrict__ counters)
             r.o = mk(a.x, a.y, a.z);
             r.d = mk(a.w, b.x, b.y);
             tree = __float_as_int(b.w);
-            hh = trace(S, r, b.z, cnt);
+            hh = trace(S, r, b.z, cnt, A.ocl);
             tir = hh.refr > 0 && !hh.refr_ray_ok;
             if (tir && L < 5) cnt.tir++;                // node index < 31 (:398)
             A.lcol[L][q] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
@@ -641,7 +651,7 @@ tir_kernel(WfArgs A, int L, const float *__restrict__ sx_tab, const float *__res
         if (!found) {
             const int sub = tree / A.npix, pix = tree % A.npix;
             const int x = pix % A.w, y = A.row_begin + pix / A.w;
-            r = primary(sub, sx_tab[x], sy_tab[y], DX, DY);
+            r = primary(sub, sx_tab[x], sy_tab[y], DX, DY, A.side);
         }
         const int seg = tree & (NSEG - 1);
         const int k = atomicAdd(&CNT(A, C_SEG + (L + 1) * NSEG + seg), 1);
@@ -657,10 +667,11 @@ tir_kernel(WfArgs A, int L, const float *__restrict__ sx_tab, const float *__res
 // (Beer factor from the node's own distance and colour, unless TIR) first,
 // then the reflection child (colour x refl).
 __device__ __forceinline__ float4 accumulate(const Scene &S, float4 pc, int pinfo, int2 ch,
-                                             const float4 *__restrict__ ccol)
+                                             const float4 *__restrict__ ccol, bool ocl)
 {
     const float4 pm = S.mat0[pinfo & 0xff];
-    if (ch.y >= 0) {
+    const auto refr = [&]() {
+        if (ch.y < 0) return;
         const float4 cc = ccol[ch.y];
         float ax = cc.x, ay = cc.y, az = cc.z;
         if (!(pinfo & INFO_TIR)) {
@@ -670,12 +681,20 @@ __device__ __forceinline__ float4 accumulate(const Scene &S, float4 pc, int pinf
             az = cc.z * rtm::expf(pm.z * 0.15f * nd);
         }
         pc.x += ax; pc.y += ay; pc.z += az;
-    }
-    if (ch.x >= 0) {
+    };
+    const auto refl = [&]() {
+        if (ch.x < 0) return;
         const float4 cc = ccol[ch.x];
         pc.x += cc.x * pm.x * pm.w;
         pc.y += cc.y * pm.y * pm.w;
         pc.z += cc.z * pm.z * pm.w;
+    };
+    if (ocl) {                     // openCLcode.cl:199-233: reflection child first
+        refl();
+        refr();
+    } else {
+        refr();
+        refl();
     }
     return pc;
 }
@@ -693,7 +712,7 @@ backacc_kernel(WfArgs A, int L)
         if (lane >= nvalid) continue;
         const int2 ch = A.lchild[L][q];
         if (ch.x < 0 && ch.y < 0) continue;
-        A.lcol[L][q] = accumulate(S, A.lcol[L][q], A.linfo[L][q], ch, A.lcol[L + 1]);
+        A.lcol[L][q] = accumulate(S, A.lcol[L][q], A.linfo[L][q], ch, A.lcol[L + 1], A.ocl);
     }
 }
 
@@ -710,16 +729,17 @@ final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
     if (x >= A.w || y >= row_end) return;
     const int pix = (y - A.row_begin) * A.w + x;
     float tr = 0.f, tg = 0.f, tb = 0.f;
-    for (int sub = 0; sub < 9; sub++) {
+    for (int sub = 0; sub < A.nsub; sub++) {
         const int tree = sub * A.npix + pix;
         float4 c0 = A.rcol[tree];
         if (A.fixflag[tree] == 0) {
             const int2 ch = A.rchild[tree];
-            if (ch.x >= 0 || ch.y >= 0) c0 = accumulate(S, c0, A.rinfo[tree], ch, A.lcol[1]);
+            if (ch.x >= 0 || ch.y >= 0) c0 = accumulate(S, c0, A.rinfo[tree], ch, A.lcol[1], A.ocl);
         }
         tr += c0.x; tg += c0.y; tb += c0.z;
     }
-    int red = (int)(tr * 28.0f), green = (int)(tg * 28.0f), blue = (int)(tb * 28.0f);
+    const float scale = A.ocl ? 64.0f : 28.0f;            // 256/4 (openCLcode.cl:238) or 256/9 (:517)
+    int red = (int)(tr * scale), green = (int)(tg * scale), blue = (int)(tb * scale);
     if (red > 255) red = 255;
     if (green > 255) green = 255;
     if (blue > 255) blue = 255;
@@ -759,7 +779,7 @@ fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict
         const int x = pix % A.w, y = A.row_begin + pix / A.w;
         NodeStore ns;
         unsigned long long todo = 1, traced = 0;
-        const ray3 root = primary(sub, sx_tab[x], sy_tab[y], DX, DY);
+        const ray3 root = primary(sub, sx_tab[x], sy_tab[y], DX, DY, A.side);
         ray3 cur_refr = root;          // the caller's refr_Ray variable (:373-374)
         while (todo) {
             const int i = __builtin_ctzll(todo);
@@ -783,7 +803,7 @@ fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict
                 }
             }
             Counts c1 = {0, 0, 0, 0};
-            Hit hh = trace(S, r, rin, c1);
+            Hit hh = trace(S, r, rin, c1, A.ocl);
             const bool tir = hh.refr > 0 && !hh.refr_ray_ok;
             if (wf < 0) {                  // not traced by the level pass: count it here
                 cnt.traced += c1.traced; cnt.shadow += c1.shadow; cnt.tests += c1.tests;
@@ -806,31 +826,34 @@ fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict
                 }
             }
         }
-        // Back-accumulation (:476-511): children in decreasing index order,
-        // refraction child (even) before reflection child (odd).
-        unsigned long long m = traced & ~1ull;
-        while (m) {
-            const int c = 63 - __builtin_clzll(m);
-            m &= ~(1ull << c);
-            const int p = (c - 1) >> 1;
-            const float4 cc = ns.col[c];
+        // Back-accumulation (:476-511): parents in decreasing index order; per
+        // parent the refraction child then the reflection child (the CPU
+        // path) or the reverse (openCLcode.cl:199-233).
+        for (int p = NODES / 2 - 1; p >= 0; p--) {
+            if (!((traced >> p) & 1ull)) continue;
             float4 pc = ns.col[p];
             const int pinfo = ns.info[p];
             const float4 pm = S.mat0[pinfo & 0xff];
-            float ax = cc.x, ay = cc.y, az = cc.z;
-            if (!(c & 1)) {
-                if (!(pinfo & INFO_TIR)) {
-                    const float nd = -pc.w;
-                    ax = cc.x * rtm::expf(pm.x * 0.15f * nd);
-                    ay = cc.y * rtm::expf(pm.y * 0.15f * nd);
-                    az = cc.z * rtm::expf(pm.z * 0.15f * nd);
+            for (int k = 0; k < 2; k++) {
+                const bool refr_side = A.ocl ? (k == 1) : (k == 0);
+                const int c = refr_side ? 2 * p + 2 : 2 * p + 1;
+                if (!((traced >> c) & 1ull)) continue;
+                const float4 cc = ns.col[c];
+                float ax = cc.x, ay = cc.y, az = cc.z;
+                if (refr_side) {
+                    if (!(pinfo & INFO_TIR)) {
+                        const float nd = -pc.w;
+                        ax = cc.x * rtm::expf(pm.x * 0.15f * nd);
+                        ay = cc.y * rtm::expf(pm.y * 0.15f * nd);
+                        az = cc.z * rtm::expf(pm.z * 0.15f * nd);
+                    }
+                } else {
+                    ax = cc.x * pm.x * pm.w;
+                    ay = cc.y * pm.y * pm.w;
+                    az = cc.z * pm.z * pm.w;
                 }
-            } else {
-                ax = cc.x * pm.x * pm.w;
-                ay = cc.y * pm.y * pm.w;
-                az = cc.z * pm.z * pm.w;
+                pc.x += ax; pc.y += ay; pc.z += az;
             }
-            pc.x += ax; pc.y += ay; pc.z += az;
             ns.col[p] = pc;
         }
         A.rcol[tree] = ns.col[0];
@@ -856,6 +879,30 @@ constexpr int SLOT_WF = 6;      // rtrt scratch slot of the wavefront arena
 // m_SX / m_SY tables (Engine_InitRender raytracer.cpp:278-294, then the
 // sequential m_SX += m_DX (:524) and m_SY += m_DY (:526)) -- host float adds,
 // uploaded once per frame size into the device state's SLOT_VIEW buffer.
+constexpr int SLOT_VIEW_OCL = 5;   // SX = WX1 + x*DX, SY = WY1 + y*DY (openCLcode.cl:22-23)
+
+int view_tables_ocl(rtrt::DeviceState &st, int w, int h, const float **d_sx, const float **d_sy)
+{
+    void *d = nullptr;
+    int rc = rtrt::scratch(st, SLOT_VIEW_OCL, sizeof(float) * ((size_t)w + h), &d);
+    if (rc) return rc;
+    if (st.vto_w != w || st.vto_h != h) {
+        const float WX1 = -3.0f, WX2 = 3.0f, WY1 = 2.25f, WY2 = -2.25f;
+        const float DX = (WX2 - WX1) / w;
+        const float DY = (WY2 - WY1) / h;
+        float *tab = new float[(size_t)w + h];
+        for (int x = 0; x < w; x++) tab[x] = WX1 + x * DX;
+        for (int y = 0; y < h; y++) tab[w + y] = WY1 + y * DY;
+        hipError_t e = hipMemcpy(d, tab, sizeof(float) * ((size_t)w + h), hipMemcpyHostToDevice);
+        delete[] tab;
+        if (e != hipSuccess) return rtrt::fail_hip(e, "whitted view tables");
+        st.vto_w = w; st.vto_h = h;
+    }
+    *d_sx = (const float *)d;
+    *d_sy = (const float *)d + w;
+    return RT_OK;
+}
+
 int view_tables(rtrt::DeviceState &st, int w, int h, const float **d_sx, const float **d_sy)
 {
     void *d = nullptr;
@@ -884,10 +931,10 @@ int view_tables(rtrt::DeviceState &st, int w, int h, const float **d_sx, const f
 
 // Device arena of the wavefront pass (scratch slot SLOT_WF, grow-only):
 // per tree a root record, per level 1..5 a queue of capacity = #trees.
-int wavefront_arena(rtrt::DeviceState &st, int w, int rows, rt::whitted::WfArgs *A)
+int wavefront_arena(rtrt::DeviceState &st, int w, int rows, int nsub, rt::whitted::WfArgs *A)
 {
     using namespace rt::whitted;
-    const size_t T = (size_t)w * rows * 9;
+    const size_t T = (size_t)w * rows * nsub;
     if (T > (size_t)0x7fffffff / 2) return rtrt::fail(RT_ERR_INVALID, "rtw: frame too large");
     // Queue capacity per level: one slot per tree.  RT_WHITTED_QUEUE_CAP
     // lowers it (test hook: exercises the overflow -> fixup path).
@@ -966,6 +1013,35 @@ int launch_wavefront(const rt_primitive *d_prims, int nprims, const rt::whitted:
     return rtrt::check_launch("rtw wavefront kernels");
 }
 
+
+int render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int w, int h, int row_begin,
+                 int row_end, uint64_t *d_counters, void *stream, bool ocl)
+{
+    rtrt::DeviceState *st;
+    int rc = rtrt::state(&st);
+    if (rc) return rc;
+    const float *d_sx, *d_sy;
+    rc = ocl ? view_tables_ocl(*st, w, h, &d_sx, &d_sy) : view_tables(*st, w, h, &d_sx, &d_sy);
+    if (rc) return rc;
+    const float DX = (3.0f - -3.0f) / w, DY = (-2.25f - 2.25f) / h;    // Engine_InitRender / openCLcode.cl:20-21
+    const int rows = row_end - row_begin;
+    rt::whitted::WfArgs A;
+    const int side = ocl ? 2 : 3;
+    rc = wavefront_arena(*st, w, rows, side * side, &A);
+    if (rc) return rc;
+    A.row_begin = row_begin;
+    A.side = side;
+    A.nsub = side * side;
+    A.ocl = ocl;
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long *cnt = (unsigned long long *)d_counters;
+    hipError_t e = hipMemsetAsync(A.count, 0, sizeof(int) * rt::whitted::C_TOTAL * rt::whitted::CSTRIDE, s);
+    if (e == hipSuccess) e = hipMemsetAsync(A.fixflag, 0, sizeof(int) * (size_t)A.ntrees, s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async memset");
+    if (cnt) return launch_wavefront<true>(d_prims, nprims, A, w, rows, row_end, d_sx, d_sy, DX, DY, cnt, s, d_xrgb);
+    return launch_wavefront<false>(d_prims, nprims, A, w, rows, row_end, d_sx, d_sy, DX, DY, cnt, s, d_xrgb);
+}
+
 }  // namespace
 
 extern "C" int rtw_render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int w,
@@ -976,26 +1052,51 @@ extern "C" int rtw_render_async(const rt_primitive *d_prims, int nprims, uint32_
         return rtrt::fail(RT_ERR_INVALID, "rtw_render_async: bad arguments");
     if (row_begin < 20 || row_end > h || row_begin >= row_end)
         return rtrt::fail(RT_ERR_INVALID, "rtw_render_async: rows must satisfy 20 <= row_begin < row_end <= h");
+    return render_async(d_prims, nprims, d_xrgb, w, h, row_begin, row_end, d_counters, stream, false);
+}
+
+extern "C" int rtw_render_ocl_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int w, int h,
+                                    uint64_t *d_counters, void *stream)
+{
+    if (!d_prims || !d_xrgb || nprims < 1 || nprims > rt::whitted::MAXP || w < 1 || h < 1)
+        return rtrt::fail(RT_ERR_INVALID, "rtw_render_ocl_async: bad arguments");
+    const int row_end = std::min(h, 530);
+    if (row_end <= 20) return RT_OK;                 // the kernel's window is empty
+    return render_async(d_prims, nprims, d_xrgb, w, h, 20, row_end, d_counters, stream, true);
+}
+
+extern "C" int rtw_render_ocl(const rt_primitive *prims, int nprims, uint32_t *xrgb, int w, int h,
+                              uint64_t *counters)
+{
+    if (!prims || !xrgb || nprims < 1 || nprims > rt::whitted::MAXP || w < 1 || h < 1)
+        return rtrt::fail(RT_ERR_INVALID, "rtw_render_ocl: bad arguments");
+    const int row_end = std::min(h, 530);
+    if (row_end <= 20) {
+        if (counters) counters[0] = counters[1] = counters[2] = counters[3] = 0;
+        return RT_OK;
+    }
     rtrt::DeviceState *st;
     int rc = rtrt::state(&st);
     if (rc) return rc;
-    const float *d_sx, *d_sy;
-    rc = view_tables(*st, w, h, &d_sx, &d_sy);
+    const size_t frame_bytes = sizeof(uint32_t) * (size_t)w * h;
+    void *d_prims, *d_frame, *d_cnt;
+    if ((rc = rtrt::scratch(*st, 0, sizeof(rt_primitive) * nprims, &d_prims))) return rc;
+    if ((rc = rtrt::scratch(*st, 1, frame_bytes, &d_frame))) return rc;
+    if ((rc = rtrt::scratch(*st, 2, 4 * sizeof(uint64_t), &d_cnt))) return rc;
+    hipStream_t s = st->stream;
+    hipError_t e = hipMemcpyAsync(d_prims, prims, sizeof(rt_primitive) * nprims, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && counters) e = hipMemsetAsync(d_cnt, 0, 4 * sizeof(uint64_t), s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_ocl H2D");
+    rc = render_async((const rt_primitive *)d_prims, nprims, (uint32_t *)d_frame, w, h, 20, row_end,
+                      counters ? (uint64_t *)d_cnt : nullptr, s, true);
     if (rc) return rc;
-    const int rows = row_end - row_begin;
-    rt::whitted::WfArgs A;
-    rc = wavefront_arena(*st, w, rows, &A);
-    if (rc) return rc;
-    A.row_begin = row_begin;
-    hipStream_t s = (hipStream_t)stream;
-    unsigned long long *cnt = (unsigned long long *)d_counters;
-    hipError_t e = hipMemsetAsync(A.count, 0, sizeof(int) * rt::whitted::C_TOTAL * rt::whitted::CSTRIDE, s);
-    if (e == hipSuccess) e = hipMemsetAsync(A.fixflag, 0, sizeof(int) * (size_t)A.ntrees, s);
-    if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async memset");
-    if (cnt) return launch_wavefront<true>(d_prims, nprims, A, w, rows, row_end, d_sx, d_sy, st->vt_DX, st->vt_DY,
-                                           cnt, s, d_xrgb);
-    return launch_wavefront<false>(d_prims, nprims, A, w, rows, row_end, d_sx, d_sy, st->vt_DX, st->vt_DY, cnt,
-                                   s, d_xrgb);
+    const size_t off = sizeof(uint32_t) * (size_t)20 * w, len = sizeof(uint32_t) * (size_t)(row_end - 20) * w;
+    e = hipMemcpyAsync((char *)xrgb + off, (char *)d_frame + off, len, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && counters)
+        e = hipMemcpyAsync(counters, d_cnt, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_ocl D2H");
+    return RT_OK;
 }
 
 extern "C" int rtw_render(const rt_primitive *prims, int nprims, uint32_t *xrgb, int w, int h,

@@ -40,6 +40,20 @@ def whitted_render(w, h, row_begin=20, row_end=None, prims=None, nprims=None, fr
     return (frame, list(cnt)) if counters else frame
 
 
+def whitted_render_ocl(w, h, prims=None, nprims=None, frame=None, counters=False):
+    """The reference's OpenCL kernel semantics (raytrace_kernel of
+    openCLcode.cl): rows [20, min(530, h)) of a uint32 [h, w] frame."""
+    if prims is None:
+        prims, nprims = scenes.whitted_scene()
+    if frame is None:
+        frame = np.zeros((h, w), dtype=np.uint32)
+    assert frame.dtype == np.uint32 and frame.shape == (h, w) and frame.flags.c_contiguous
+    cnt = (C.c_uint64 * 4)()
+    check(lib().rtw_render_ocl(C.addressof(prims), nprims, frame.ctypes.data, w, h,
+                               C.addressof(cnt) if counters else None))
+    return (frame, list(cnt)) if counters else frame
+
+
 class SmallptFrame:
     """Progressive smallpt frame state: colors / seeds / pixels exactly as
     smallptGPU.cpp's AllocateBuffers lays them out, and currentSample."""

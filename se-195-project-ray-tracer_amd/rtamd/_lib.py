@@ -16,7 +16,7 @@ SPT_PATH_TRACING, SPT_DIRECT_LIGHTING = 0, 1
 
 # Every symbol include/rt_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = ("rt_last_error", "rt_device_count", "rt_set_device", "rt_release", "rt_cached_bytes",
-           "rtw_render", "rtw_render_async", "spt_render", "spt_render_async", "spt_seed_fill",
+           "rtw_render", "rtw_render_async", "rtw_render_ocl", "rtw_render_ocl_async", "spt_render", "spt_render_async", "spt_seed_fill",
            "spt_scene_create", "spt_scene_destroy", "spt_scene_render_async")
 
 
@@ -70,6 +70,8 @@ def lib():
     L.rt_cached_bytes.restype = C.c_size_t
     L.rtw_render.argtypes = [vp, i, vp, i, i, i, i, u64p]
     L.rtw_render_async.argtypes = [vp, i, vp, i, i, i, i, u64p, vp]
+    L.rtw_render_ocl.argtypes = [vp, i, vp, i, i, u64p]
+    L.rtw_render_ocl_async.argtypes = [vp, i, vp, i, i, u64p, vp]
     L.spt_render.argtypes = [vp, u, vp, vp, vp, vp, i, i, i, i, i, u64p]
     L.spt_render_async.argtypes = [vp, u, vp, vp, vp, vp, vp, i, i, i, i, i, i, i, u64p, vp]
     L.spt_seed_fill.argtypes = [vp, C.c_size_t, u]

@@ -31,6 +31,20 @@ def test_whitted_shim_matches_cpu_path(oracle, tmp_path):
     assert (got == ref).all()
 
 
+def test_whitted_shim_opencl_semantics(oracle, tmp_path):
+    """RT_WHITTED_SEMANTICS=opencl: the shim computes raytrace_kernel's frame."""
+    _build()
+    w, h = 800, 600
+    out = tmp_path / "frame.bin"
+    env = dict(os.environ, RT_WHITTED_SEMANTICS="opencl")
+    r = subprocess.run([os.path.join(NATIVE, "whitted_app"), str(w), str(h), str(out)],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(out, dtype=np.uint32).reshape(h, w)
+    ref, _ = oracle.whitted_render_ocl(w, h, nthreads=8)
+    assert (got[20:530] == ref[20:530]).all()
+
+
 def test_smallpt_shim_matches_cpu_path(oracle, tmp_path):
     _build()
     w, h, passes = 320, 240, 5

@@ -67,3 +67,18 @@ def test_tir_trees_counted_once(rt, oracle):
     _, rc = oracle.whitted_render(640, 480, nthreads=8)
     _, gc = rt.whitted_render(640, 480, counters=True)
     assert rc[3] == 1056 and gc == rc
+
+
+@pytest.mark.parametrize("w,h", [(640, 480), (800, 600), (1920, 1080), (97, 131)])
+def test_opencl_semantics_bit_exact(rt, oracle, w, h):
+    """rtw_render_ocl (raytrace_kernel of openCLcode.cl) vs the oracle's
+    restatement of the same kernel: bit-exact frame and counters."""
+    ref, rc = oracle.whitted_render_ocl(w, h, nthreads=8)
+    got, gc = rt.whitted_render_ocl(w, h, counters=True)
+    assert (got == ref).all() and gc == rc
+
+
+def test_opencl_semantics_differs_from_cpu_path(rt):
+    a = rt.whitted_render_ocl(640, 480)
+    b = rt.whitted_render(640, 480)
+    assert (a[20:410] != b[20:410]).any() and (a[:20] == 0).all()
