@@ -51,9 +51,9 @@ def lib():
             build()
         L = C.CDLL(path)
         L.orw_scene_init.argtypes = [C.POINTER(Primitive), C.c_int]
-        L.orw_render.argtypes = [C.POINTER(Primitive), C.c_int, C.c_void_p, C.c_int, C.c_int,
+        L.orw_render.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
                                  C.c_int, C.c_int, _u64p, C.c_int]
-        L.orw_render_ocl.argtypes = [C.POINTER(Primitive), C.c_int, C.c_void_p, C.c_int, C.c_int, _u64p, C.c_int]
+        L.orw_render_ocl.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, _u64p, C.c_int]
         L.orw_primitive_intersect.argtypes = [C.POINTER(Primitive), C.c_void_p, C.POINTER(C.c_float)]
         L.orw_primitive_normal.argtypes = [C.POINTER(Primitive), C.c_void_p, C.c_void_p]
         L.ors_cornell.argtypes = [C.POINTER(Sphere), C.c_int]
@@ -92,7 +92,7 @@ def whitted_render(w, h, row_begin=20, row_end=None, nthreads=1, prims=None, n=N
         row_end = h - 70
     frame = np.zeros((h, w), dtype=np.uint32)
     cnt = (C.c_uint64 * 4)()
-    lib().orw_render(prims, n, frame.ctypes.data, w, h, row_begin, row_end, cnt, nthreads)
+    lib().orw_render(C.addressof(prims), n, frame.ctypes.data, w, h, row_begin, row_end, cnt, nthreads)
     return frame, list(cnt)
 
 
@@ -103,7 +103,7 @@ def whitted_render_ocl(w, h, nthreads=1, prims=None, n=None):
         prims, n = whitted_scene()
     frame = np.zeros((h, w), dtype=np.uint32)
     cnt = (C.c_uint64 * 4)()
-    lib().orw_render_ocl(prims, n, frame.ctypes.data, w, h, cnt, nthreads)
+    lib().orw_render_ocl(C.addressof(prims), n, frame.ctypes.data, w, h, cnt, nthreads)
     return frame, list(cnt)
 
 

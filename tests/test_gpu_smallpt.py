@@ -192,3 +192,36 @@ def test_bvh_equals_full_scan_random_scenes(rt, monkeypatch, seed, mode):
     cam.target = rt.Vec3(0.0, 0.0, 0.0)
     rt.scenes.update_camera(cam, 160, 120)
     _bvh_vs_scan(rt, monkeypatch, S, n, cam, 160, 120, 4, mode)
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13, 14, 15, 16])
+def test_random_scenes_vs_oracle(rt, oracle, seed):
+    """Random scenes (random sphere count, sizes, materials, lights, some
+    overlapping, random camera) at ragged sizes, split progressive passes and
+    both estimators, against the oracle: bit-exact HDR, seeds, pixels, counts."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(3, 40))
+    S = (rt.Sphere * n)()
+    for i in range(n):
+        big = rng.random() < 0.2
+        rad = float(10 ** rng.uniform(2, 4)) if big else float(10 ** rng.uniform(-1.5, 1.2))
+        c = rng.uniform(-60, 60, 3)
+        if big:
+            ax = int(rng.integers(0, 3))
+            c[ax] = np.sign(rng.standard_normal()) * (rad + rng.uniform(20, 80))
+        light = rng.random() < 0.15 or i == 0
+        e = tuple(rng.uniform(1, 15, 3)) if light else (0.0, 0.0, 0.0)
+        refl = int(rng.choice([0, 0, 0, 1, 2]))
+        rt.scenes._sphere(S[i], rad, tuple(c), e, tuple(rng.uniform(0.1, 0.95, 3)), refl)
+    w, h = int(rng.integers(24, 90)), int(rng.integers(16, 70))
+    cam = rt.Camera()
+    cam.orig = rt.Vec3(*map(float, rng.uniform(-20, 20, 3)))
+    cam.target = rt.Vec3(*map(float, rng.uniform(-20, 20, 3)))
+    rt.scenes.update_camera(cam, w, h)
+    mode = int(seed % 2)
+    steps = [int(rng.integers(1, 4)), int(rng.integers(1, 4))]
+    f = rt.SmallptFrame(w, h, spheres=S, nspheres=n, camera=cam, mode=mode)
+    for k in steps:
+        f.render(k)
+    ref = _oracle_frame(oracle, w, h, steps, mode=mode, spheres=(S, n), cam=cam)
+    _check((f.colors, f.seeds, f.pixels, f.counters), ref)
