@@ -122,19 +122,24 @@ __device__ __forceinline__ int query(const G &geo, const ray3 &r, float &t, int 
 // visits, and skips a sphere only when d_i provably cannot matter, returns
 // identical bits.
 //
-// Skipping rule.  For a sphere inside box B (centre C, half-diagonal R), a
-// float distance t* puts the point o + t*.d within m = ALPHA * (|o - C| + R)
-// + BETA of B: the float formula's root differs from the geometric one by at
-// most sqrt(|det error|) + |b error| <= ~1.1e-3 * |op| (det = b*b - op.op +
-// rad^2 cancels in float; |op| <= |o - C| + R), and a direction of length
-// 1 +- delta moves the formula's roots by <= sqrt(2 delta) * |op| (rays are
-// normalised or built from unit vectors: delta < 1e-6 -> 1.4e-3 * |op|);
-// ALPHA = 1/64 is more than three times the sum.  So a node whose box,
-// grown by m on every side, is not crossed by the ray between 0 and lim
-// (the current nearest distance, or maxt) holds no sphere that could be
-// taken; its spheres are skipped.  The slab test's own rounding (relative
-// 1e-6, approximate reciprocals and square root) is covered by the same
-// slack.
+// Skipping rule.  For a sphere (radius r, |c - o| = |op|) inside box B
+// (centre C, half-diagonal R), a float distance t* puts the point o + t*.d
+// within  m = 1.04e-3 * (|op| + r) + sqrt(e) * t*  of the sphere, hence of B:
+//   * the float root b -+ sqrt(det) differs from the geometric one by at most
+//     sqrt(|det error|) + |b error|, with |det error| <= ~18u max(|op|, r)^2
+//     (u = 2^-24; det = b*b - op.op + rad^2 cancels in float) -> 1.04e-3 *
+//     max(|op|, r);
+//   * a direction with |d|^2 = 1 + e puts the formula's roots on a sphere of
+//     radius sqrt(r^2 + e t*^2), i.e. sqrt(e) * t* further out.
+// With |op| <= |o - C| + R, r <= R and t* <= |o - C| + 2R this is below
+// alpha * |o - C| + BVH_ALPHA_R * R + BETA for alpha = 1/128 when e < 2^-20
+// (rays here are normalised or built from unit vectors: e ~ 1e-7), alpha =
+// 1/16 when e < 2^-9, and no culling at all beyond; each is more than three
+// times the bound.  So a node whose box, grown by m on every side, is not
+// crossed by the ray between 0 and lim (the current nearest distance, or
+// maxt) holds no sphere that could be taken; its spheres are skipped.  BETA
+// and the same slack absorb the slab test's own rounding (approximate
+// reciprocals and square root, relative ~1e-6) and the box corners'.
 // Spheres whose radius dwarfs the rest (the ground) are tested first, for
 // every ray, outside the hierarchy.
 struct BvhView {
@@ -145,7 +150,7 @@ struct BvhView {
     const int *aid;
     int nalways, nnodes;
 };
-constexpr float BVH_ALPHA = 1.f / 64.f;
+constexpr float BVH_ALPHA_R = 1.f / 64.f;   // per node, with BETA, in the node record
 
 // One ray query through the hierarchy.  Nearest hit (shadow = false): t in
 // = 1e20f, out = nearest distance, returns its index (highest on ties) or
@@ -177,6 +182,8 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
     const float dz = fabsf(r.d.z) < 1e-30f ? copysignf(1e-30f, r.d.z) : r.d.z;
     const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
     const float ax = fabsf(ix), ay = fabsf(iy), az = fabsf(iz);
+    const float e = fabsf(r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z - 1.f);
+    const float alpha = e < 0x1p-20f ? 1.f / 128.f : (e < 0x1p-9f ? 1.f / 16.f : 1e30f);
     // Layout of this ray's direction octant: near children first.
     const float4 *nodes = B.node + 2 * (size_t)B.nnodes *
                                        ((dx < 0.f ? 1 : 0) | (dy < 0.f ? 2 : 0) | (dz < 0.f ? 4 : 0));
@@ -202,7 +209,7 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
             const float lim = shadow ? maxt : t;
             const float cx = a.x - r.o.x, cy = a.y - r.o.y, cz = a.z - r.o.z;
             const float dist = __builtin_amdgcn_sqrtf(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, cz * cz)));
-            const float m = __builtin_fmaf(BVH_ALPHA, dist, b.w);
+            const float m = __builtin_fmaf(alpha, dist, b.w);
             const float tcx = cx * ix, tcy = cy * iy, tcz = cz * iz;                // slab centres
             const float hx = (b.x + m) * ax, hy = (b.y + m) * ay, hz = (b.z + m) * az;  // slab half-widths
             const float tn = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
@@ -636,7 +643,7 @@ struct BvhBuild {
             d2 += (double)(nd.hi[k] - nd.lo[k]) * (nd.hi[k] - nd.lo[k]);
             mag = std::max(mag, (double)std::max(fabsf(nd.lo[k]), fabsf(nd.hi[k])));
         }
-        nd.margin = (float)(rt::smallpt::BVH_ALPHA * 0.5 * sqrt(d2) + 1e-3 + 1e-5 * mag);
+        nd.margin = (float)(rt::smallpt::BVH_ALPHA_R * 0.5 * sqrt(d2) + 1e-3 + 1e-5 * mag);
         const int n = hi - lo;
         if (n <= BVH_LEAF) {
             nd.first = lo;
