@@ -39,7 +39,7 @@ FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: peak FP32 vector
 W, H, SPP = 1920, 1080, 64
 
 
-BENCH_KERNEL = "rt::smallpt::render_kernel<false, false, true>"
+BENCH_KERNEL = "rt::smallpt::render_kernel<false, false, 0>"
 
 
 def pmc_digest(kernel):

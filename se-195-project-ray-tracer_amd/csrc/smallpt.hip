@@ -151,12 +151,21 @@ struct BvhView {
     int nalways, nnodes;
 };
 constexpr float BVH_ALPHA_R = 1.f / 64.f;   // per node, with BETA, in the node record
+constexpr int BVH_LEAF_MAX = 4;             // spheres per leaf (host build: BVH_LEAF)
 
 // One ray query through the hierarchy.  Nearest hit (shadow = false): t in
 // = 1e20f, out = nearest distance, returns its index (highest on ties) or
 // -1.  Any hit (shadow = true): t = maxt, returns an occluder index or -1;
 // with COUNT the highest one (IntersectP's early-exit position, for the test
 // counter), without COUNT the traversal stops at the first.
+//
+// The walk is latency-bound (one dependent node load per step, L1/L2 hits):
+// every step loads both halves of the node record together and runs the slab
+// test before branching on the node kind -- leaves are tested against their
+// own grown box too -- and a leaf issues the loads of all its spheres and
+// indices before the first test, so a step costs one memory latency (a first
+// form that branched on the link word first and loaded per sphere paid two
+// to five: configs[4] 11.1 -> 8.5 ms per 4 spp).
 template <bool COUNT>
 __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
 {
@@ -191,32 +200,46 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
     while (node < B.nnodes) {
         const float4 a = nodes[2 * node], b = nodes[2 * node + 1];
         const int link = __float_as_int(a.w);
-        if (link < 0) {                                  // leaf: first | count << 24
-            const int info = ~link;
-            const int f = info & 0xffffff, e = f + (info >> 24);
-            for (int j = f; j < e; j++) {
-                const float d = sphere_hit(B.geo[j], r);
-                const int i = B.id[j];
-                if (shadow) {
-                    if (d < maxt && i > id) id = i;
-                } else if (d < t || (d == t && i > id)) {
-                    t = d;
-                    id = i;
+        const float lim = shadow ? maxt : t;
+        const float cx = a.x - r.o.x, cy = a.y - r.o.y, cz = a.z - r.o.z;
+        const float dist = __builtin_amdgcn_sqrtf(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, cz * cz)));
+        const float m = __builtin_fmaf(alpha, dist, b.w);
+        const float tcx = cx * ix, tcy = cy * iy, tcz = cz * iz;                // slab centres
+        const float hx = (b.x + m) * ax, hy = (b.y + m) * ay, hz = (b.z + m) * az;  // slab half-widths
+        const float tn = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
+        const float tf = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
+        const bool cross = tn <= tf && tf >= 0.f && tn <= lim;
+        int next = cross ? node + 1 : link;
+        if (link < 0) {                                  // leaf ~(first | count << 24); escape = next node
+            next = node + 1;
+            if (cross) {
+                const int info = ~link;
+                const int f = info & 0xffffff, c = info >> 24;
+                float4 g[BVH_LEAF_MAX];
+                int gi[BVH_LEAF_MAX];
+#pragma unroll
+                for (int q = 0; q < BVH_LEAF_MAX; q++) {  // all loads first: one latency per leaf
+                    const int j = f + (q < c ? q : 0);
+                    g[q] = B.geo[j];
+                    gi[q] = B.id[j];
                 }
+#pragma unroll
+                for (int q = 0; q < BVH_LEAF_MAX; q++) {
+                    if (q < c) {
+                        const float d = sphere_hit(g[q], r);
+                        const int i = gi[q];
+                        if (shadow) {
+                            if (d < maxt && i > id) id = i;
+                        } else if (d < t || (d == t && i > id)) {
+                            t = d;
+                            id = i;
+                        }
+                    }
+                }
+                if (!COUNT && shadow && id >= 0) next = B.nnodes;
             }
-            node = (!COUNT && shadow && id >= 0) ? B.nnodes : node + 1;   // a leaf's escape is the next node
-        } else {                                         // inner node: link = escape
-            const float lim = shadow ? maxt : t;
-            const float cx = a.x - r.o.x, cy = a.y - r.o.y, cz = a.z - r.o.z;
-            const float dist = __builtin_amdgcn_sqrtf(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, cz * cz)));
-            const float m = __builtin_fmaf(alpha, dist, b.w);
-            const float tcx = cx * ix, tcy = cy * iy, tcz = cz * iz;                // slab centres
-            const float hx = (b.x + m) * ax, hy = (b.y + m) * ay, hz = (b.z + m) * az;  // slab half-widths
-            const float tn = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
-            const float tf = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
-            const bool cross = tn <= tf && tf >= 0.f && tn <= lim;
-            node = cross ? node + 1 : link;
         }
+        node = next;
     }
     return id;
 }
@@ -590,7 +613,7 @@ void launch_mode(bool dl, bool count, dim3 grid, hipStream_t s, const spt_scene 
 }
 
 // ---- hierarchy build (host) for scenes of >= BVH_MIN spheres
-constexpr int BVH_MIN = 256, BVH_LEAF = 4, BVH_MAX_ALWAYS = 16;
+constexpr int BVH_MIN = 256, BVH_LEAF = rt::smallpt::BVH_LEAF_MAX, BVH_MAX_ALWAYS = 16;
 
 struct HostNode {
     float lo[3], hi[3];

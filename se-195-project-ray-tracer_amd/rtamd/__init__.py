@@ -72,13 +72,15 @@ class SmallptFrame:
         self.current_sample = 0
         self.counters = [0, 0, 0, 0]
 
-    def render(self, nsamples=1):
-        """nsamples successive UpdateRenderingCPU passes on the GPU."""
+    def render(self, nsamples=1, counters=True):
+        """nsamples successive UpdateRenderingCPU passes on the GPU.  With
+        counters=False no counter buffer is passed (the kernels without the
+        work counters: the ones bench.py times)."""
         cnt = (C.c_uint64 * 4)()
         check(lib().spt_render(C.addressof(self.spheres), self.nspheres, C.byref(self.camera),
                                self.colors.ctypes.data, self.seeds.ctypes.data,
                                self.pixels.ctypes.data, self.w, self.h, self.current_sample,
-                               nsamples, self.mode, C.addressof(cnt)))
+                               nsamples, self.mode, C.addressof(cnt) if counters else None))
         self.current_sample += nsamples
         self.counters = [a + b for a, b in zip(self.counters, cnt)]
         return self

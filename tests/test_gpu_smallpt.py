@@ -74,8 +74,8 @@ def test_full_size_golden(rt, oracle, key):
     w, h = map(int, res.split("x"))
     f = rt.SmallptFrame(w, h)
     spp = int(spp[:-3])
-    f.render(spp // 2)            # two launches: also exercises the first_sample > 0 path
-    f.render(spp - spp // 2)
+    f.render(spp // 2)            # two launches: also exercises the first_sample > 0 path,
+    f.render(spp - spp // 2, counters=False)   # and the uncounted kernel bench.py times
     got = (oracle.fnv1a64(f.colors), oracle.fnv1a64(f.pixels), oracle.fnv1a64(f.seeds))
     assert got == (g["colors"], g["pixels"], g["seeds"])
 
@@ -146,21 +146,25 @@ def test_async_device_paths(rt, oracle):
 
 
 def _bvh_vs_scan(rt, monkeypatch, spheres, n, cam, w, h, spp, mode=0):
-    """Renders with the hierarchy and with the full scan (RT_SPT_NO_BVH):
-    colours, seeds, pixels and counters must be identical bit for bit."""
+    """Renders with the hierarchy and with the full scan (RT_SPT_NO_BVH),
+    each with and without the work counters (the uncounted kernels stop a
+    shadow query at its first occluder): colours, seeds, pixels and counters
+    must be identical bit for bit."""
     outs = []
     for no_bvh in (False, True):
         if no_bvh:
             monkeypatch.setenv("RT_SPT_NO_BVH", "1")
         else:
             monkeypatch.delenv("RT_SPT_NO_BVH", raising=False)
-        f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n, camera=cam, mode=mode)
-        f.render(spp)
-        outs.append(f)
-    a, b = outs
-    assert np.array_equal(a.colors.view(np.uint32), b.colors.view(np.uint32))
-    assert np.array_equal(a.seeds, b.seeds) and np.array_equal(a.pixels, b.pixels)
-    assert a.counters == b.counters
+        for counted in (True, False):
+            f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n, camera=cam, mode=mode)
+            f.render(spp, counters=counted)
+            outs.append(f)
+    a = outs[0]
+    for b in outs[1:]:
+        assert np.array_equal(a.colors.view(np.uint32), b.colors.view(np.uint32))
+        assert np.array_equal(a.seeds, b.seeds) and np.array_equal(a.pixels, b.pixels)
+    assert a.counters == outs[2].counters
 
 
 def test_bvh_equals_full_scan_configs4(rt, monkeypatch):
@@ -225,3 +229,8 @@ def test_random_scenes_vs_oracle(rt, oracle, seed):
         f.render(k)
     ref = _oracle_frame(oracle, w, h, steps, mode=mode, spheres=(S, n), cam=cam)
     _check((f.colors, f.seeds, f.pixels, f.counters), ref)
+    g = rt.SmallptFrame(w, h, spheres=S, nspheres=n, camera=cam, mode=mode)
+    for k in steps:
+        g.render(k, counters=False)
+    assert (g.colors.view(np.uint32) == f.colors.view(np.uint32)).all()
+    assert (g.seeds == f.seeds).all() and (g.pixels == f.pixels).all()

@@ -20,7 +20,7 @@ seeds0 = torch.from_numpy(rtamd.scenes.seeds(W, H).view(np.int32)).to(dev)
 seeds = torch.empty_like(seeds0)
 col = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
 px = torch.zeros(W * H, dtype=torch.int32, device=dev)
-cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+cnt = torch.zeros(20, dtype=torch.int64, device=dev)   # [4..7]: RT_BVH_STATS builds
 st = torch.cuda.current_stream(dev)
 L = rtamd.lib()
 
@@ -42,3 +42,10 @@ torch.cuda.synchronize()
 ms = a.elapsed_time(b)
 print("c5 %dx%d spp=%d spheres=%d: %.1f ms, rays %d, %.1f Mrays/s, sphere tests %d" % (
     W, H, SPP, n, ms, rays, rays / ms / 1e3, int(cnt[2])))
+if int(cnt[7]):
+    q = rays
+    print("  per query: %.1f nodes, %.1f sphere tests; lane trips / (64 x wave trips) = %.3f" % (
+        int(cnt[4]) / q, int(cnt[5]) / q, int(cnt[6]) / (64 * int(cnt[7]))))
+    print("  queries with >= 128 / 512 / 2048 node visits: %d %d %d; far (leaf scan): %d" % tuple(int(v) for v in cnt[8:12]))
+    print("  >= 2048: origin-root distance <25/<50/<100/<200/<400/more: %s; shadow %d; hit %d" % (
+        [int(v) for v in cnt[12:18]], int(cnt[18]), int(cnt[19])))
