@@ -71,6 +71,7 @@ int state(DeviceState **out)
         }
         st = new DeviceState();
         st->device = dev;
+        st->cus = prop.multiProcessorCount;
         e = hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking);
         if (e != hipSuccess) { delete st; return fail_hip(e, "hipStreamCreate"); }
         g_states[dev] = st;

@@ -15,6 +15,7 @@ constexpr int SLOT_VIEW = 7;
 
 struct DeviceState {
     int device = -1;
+    int cus = 0;                       // compute units (launch shaping)
     hipStream_t stream = nullptr;      // stream of the blocking entry points
     void *buf[NSCRATCH] = {};          // grow-only device buffers
     size_t cap[NSCRATCH] = {};

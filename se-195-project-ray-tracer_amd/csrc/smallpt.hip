@@ -10,7 +10,8 @@
 // reproduced by rt_glibc_math.h), well inside the 1e-4 HDR tolerance.
 //
 // Mapping (MI355X-first, not a port of rendering_kernel.cl):
-//   * one lane per pixel, a wave per 8x8 tile, 256-thread blocks (16x16);
+//   * one lane per pixel, a wave per 8x8 tile (launch_shape: 4 or 16 waves
+//     per block, a block's waves spread over the row window);
 //   * ALL samples of a launch run in-lane with path regeneration: the per-
 //     lane loop advances one bounce per iteration and a lane whose path ended
 //     immediately starts its next sample, so a wave's cost is the max over
@@ -29,10 +30,13 @@
 namespace rt {
 namespace smallpt {
 
-constexpr int MAXS_LDS = 2048;           // LDS copy sized to n: 52 B per sphere, <= 104 KB
+constexpr int MAX_LDS_BYTES = 96 * 1024; // per-block scene copy: 48 B per sphere + 48 B per light
 constexpr float EPS = 0.01f;             // geom.h:29
 constexpr float PI_F = 3.14159265358979323846f;
 constexpr int DIFF = 0, SPEC = 1;   // REFR = 2 is the remaining case
+#ifndef RT_SPT_QUNROLL
+#define RT_SPT_QUNROLL 3
+#endif
 
 struct SphereGeo { float4 g; };          // centre.xyz, rad*rad (same float product as :42)
 
@@ -75,7 +79,7 @@ __device__ __forceinline__ float sphere_hit(float4 g, const ray3 &r)
 }
 
 // Sphere geometry for the nearest-hit / any-hit loops: LDS (per-block copy)
-// or global-memory float4 array (scenes above MAXS_LDS), runtime count.
+// or global-memory float4 array (scenes above MAX_LDS_BYTES), runtime count.
 struct DynGeo {
     const float4 *g;
     int n;
@@ -87,7 +91,7 @@ struct Scene {                // per-block LDS copy (or global view for big scen
     const float4 *geo;        // centre, rad^2 (per-lane lookups of the hit sphere)
     const float4 *emi;        // emission.xyz, refl (as int bits)
     const float4 *col;        // colour.xyz, rad
-    const int *lights;        // indices with !viszero(e), ascending
+    const float4 *lrec;       // per light (!viszero(e), ascending index): geo, col, emi
     int n, nlights;
 };
 
@@ -108,6 +112,44 @@ __device__ __forceinline__ int query(const G &geo, const ray3 &r, float &t, int 
         t = take ? d : t;
         id = take ? i : id;
         if (COUNT) first = (first < 0 && take) ? i : first;
+    }
+    return id;
+}
+
+// The same query with a branch-free sphere test and the next sphere's record
+// loaded while the current one is tested (one LDS / scalar-load latency per
+// query instead of one per sphere).  sqrt_nr is exact for det in [2^-96,
+// inf); for det < 0 or NaN it returns NaN, and NaN roots fail both "> EPS"
+// tests -- the reference's miss; for det = +inf it returns NaN where sqrtf
+// returns +inf, whose root b + inf is never "< t" for the finite t of
+// every caller -- a miss either way.  Only |det| < 2^-96 (where sqrt_nr
+// is not sqrtf, e.g. det = +-0) is unsafe: any lane that meets one in the
+// whole query has the wave redo the query with the exact per-sphere test.
+template <bool COUNT, class G>
+__device__ __forceinline__ int query_bf(const G &geo, const ray3 &r, float &t, int &first)
+{
+    const float t_in = t;
+    int id = -1;
+    bool bad = false;
+#pragma unroll RT_SPT_QUNROLL
+    for (int i = geo.count() - 1; i >= 0; i--) {
+        const float4 g = geo.at(i);
+        const float opx = g.x - r.o.x, opy = g.y - r.o.y, opz = g.z - r.o.z;
+        const float b = opx * r.d.x + opy * r.d.y + opz * r.d.z;
+        const float det = b * b - (opx * opx + opy * opy + opz * opz) + g.w;
+        bad = bad || fabsf(det) < 0x1p-96f;
+        const float sd = sqrt_nr(det);
+        const float t1 = b - sd, t2 = b + sd;
+        const float d = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
+        const bool take = d < t;
+        t = take ? d : t;
+        id = take ? i : id;
+        if (COUNT) first = (first < 0 && take) ? i : first;
+    }
+    if (wave_any(bad)) {
+        t = t_in;
+        first = -1;
+        id = query<COUNT>(geo, r, t, first);
     }
     return id;
 }
@@ -246,6 +288,30 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
 
 struct Counts { unsigned long long isect, isectp, tests, samples; };
 
+// Tools-only block profile (build with -DRT_SPT_PROF; tools/ab.py PROF=1):
+// per code block, the lanes that executed it and the wave-executions
+// (iterations in which at least one lane of the wave did).  Never in the
+// product build.
+#ifdef RT_SPT_PROF
+enum { PB_ITER, PB_SHADOW, PB_NEAREST, PB_DIFF, PB_SPEC, PB_REFR, PB_LIGHT, PB_BOUNCE, PB_DONE, PB_N };
+__device__ unsigned long long g_spt_prof[2 * PB_N];
+#define SPT_PROF(b)                                                                        \
+    do {                                                                                   \
+        prof_l[b]++;                                                                       \
+        if ((int)(threadIdx.x & 63) == __builtin_ctzll(__builtin_amdgcn_read_exec())) prof_w[b]++; \
+    } while (0)
+#else
+#define SPT_PROF(b) do {} while (0)
+#endif
+
+// Tools-only wave timeline (build with -DRT_SPT_TRACE): per wave of the grid
+// {start, end} (s_memrealtime, 100 MHz), HW_ID, XCC_ID and {sum, max} over
+// its lanes of the loop iterations, at g_spt_trace[2 * (linear block * 4 +
+// wave) + 0/1].  Never in the product build.
+#ifdef RT_SPT_TRACE
+__device__ uint4 *g_spt_trace;
+#endif
+
 // toInt, vec.h:62 (clamp macro keeps -0.0; glibc powf via rt_glibc_math.h).
 __device__ __forceinline__ int to_int(float x)
 {
@@ -253,59 +319,64 @@ __device__ __forceinline__ int to_int(float x)
     return (int)(rtm::powf(c, 1.f / 2.2f) * 255.f + .5f);
 }
 
+#ifndef RT_SPT_QV
+#define RT_SPT_QV 2         // sphere query form: 2 = query_bf, 1 = query (A/B builds)
+#endif
+#ifndef RT_SPT_QUNROLL
+#define RT_SPT_QUNROLL 3
+#endif
 #ifndef RT_SPT_MINWAVES
 #define RT_SPT_MINWAVES 1   // __launch_bounds__ min waves per SIMD (occupancy A/B builds)
 #endif
 constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2;
 
 template <bool DL, bool COUNT, int GEO>
-__global__ void __launch_bounds__(256, RT_SPT_MINWAVES)
+__global__ void __launch_bounds__(1024, RT_SPT_MINWAVES)
 render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,
               uint32_t *seeds_out, uint32_t *__restrict__ pixels, int w, int h,
-              int row_begin, int row_end, int first_sample, int nsamples,
+              int row_begin, int row_end, int tiles_x, int ntiles, int first_sample, int nsamples,
               const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
-              const float4 *__restrict__ g_col, const int *__restrict__ g_lights, int g_nlights,
+              const float4 *__restrict__ g_col, const float4 *__restrict__ g_lrec, int nlights,
               BvhView bvh, unsigned long long *__restrict__ counters)
 {
     constexpr bool LDS = GEO == GEO_LDS;
-    // Dynamic LDS carve (16-B aligned base, 16-B multiples): geo | emi | col | lights | count
+#ifdef RT_SPT_TRACE
+    const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    // Dynamic LDS carve (16-B multiples): geo | emi | col (n each) | lrec (3 per light),
+    // a copy of the scene's global SoA (spt_scene_create).
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Scene S;
     if (LDS) {
-        float4 *s_geo = (float4 *)smem;
-        float4 *s_emi = s_geo + nspheres;
-        float4 *s_col = s_emi + nspheres;
-        int *s_lights = (int *)(s_col + nspheres);
-        int &s_nl = s_lights[nspheres];
-        for (int i = threadIdx.x; i < nspheres; i += blockDim.x) {
-            const rt_sphere &q = spheres[i];
-            s_geo[i] = make_float4(q.p.x, q.p.y, q.p.z, q.rad * q.rad);
-            s_emi[i] = make_float4(q.e.x, q.e.y, q.e.z, __int_as_float(q.refl));
-            s_col[i] = make_float4(q.c.x, q.c.y, q.c.z, q.rad);
-        }
-        if (threadIdx.x == 0) {
-            int nl = 0;
-            for (int i = 0; i < nspheres; i++) {   // !viszero(e): tests e.x twice (vec.h:44)
-                const rt_sphere &q = spheres[i];
-                if (!((q.e.x == 0.f) && (q.e.x == 0.f) && (q.e.z == 0.f))) s_lights[nl++] = i;
-            }
-            s_nl = nl;
-        }
+        float4 *s = (float4 *)smem;
+        const int nrec = 3 * nspheres + 3 * nlights;
+        for (int i = threadIdx.x; i < nrec; i += blockDim.x) s[i] = g_geo[i];
         __syncthreads();
-        S.geo = s_geo; S.emi = s_emi; S.col = s_col; S.lights = s_lights; S.nlights = s_nl;
+        S.geo = s; S.emi = s + nspheres; S.col = s + 2 * nspheres; S.lrec = s + 3 * nspheres;
     } else {
-        S.geo = g_geo; S.emi = g_emi; S.col = g_col; S.lights = g_lights; S.nlights = g_nlights;
+        S.geo = g_geo; S.emi = g_emi; S.col = g_col; S.lrec = g_lrec;
     }
+    S.nlights = nlights;
     S.n = nspheres;
     const DynGeo geo{S.geo, S.n};
 
+    // 8x8 pixel tiles of the row window, one per wave; wave j of block b
+    // takes tile j * gridDim.x + b, so a block's waves sample the whole
+    // window (per-block, hence per-CU, work evens out).
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int y = row_begin + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool active = x < w && y < row_end;
+    const int tile = wave * (int)gridDim.x + (int)blockIdx.x;
+    const int x = (tile % tiles_x) * 8 + (lane & 7);
+    const int y = row_begin + (tile / tiles_x) * 8 + (lane >> 3);
+    const bool active = tile < ntiles && x < w && y < row_end;
 
     Counts cnt = {0, 0, 0, 0};
+#ifdef RT_SPT_PROF
+    unsigned prof_l[PB_N] = {}, prof_w[PB_N] = {};
+#endif
+#ifdef RT_SPT_TRACE
+    unsigned tr_iters = 0;
+#endif
     if (active) {
         const int i = (h - y - 1) * w + x;                      // smallptCPU.cpp:86
         uint32_t s0 = seeds_in[2 * (size_t)i], s1 = seeds_in[2 * (size_t)i + 1];
@@ -325,7 +396,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         v3 rad, thr;
         int depth;
         bool specular;
-        bool shadow = false;   // ray is the shadow ray of light S.lights[li]
+        bool shadow = false;   // ray is the shadow ray of light li
         v3 hit, nl;            // the DIFF vertex (SampleLights' hitPoint, normal)
         v3 lsum;               // SampleLights' running result
         float lmax = 0.f;      // shadow ray maxt (len - EPSILON)
@@ -353,6 +424,10 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         int k = 0;
         if (nsamples > 0) camera_ray();
         while (k < nsamples) {
+            SPT_PROF(PB_ITER);
+#ifdef RT_SPT_TRACE
+            tr_iters++;
+#endif
             float t = shadow ? lmax : 1e20f;
             int first = -1;
             int id;
@@ -360,14 +435,19 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 id = query_bvh<COUNT>(bvh, ray, shadow, t);
                 first = id;                 // any hit: the highest occluder (COUNT)
             } else {
+#if RT_SPT_QV == 2
+                id = query_bf<COUNT>(geo, ray, t, first);
+#else
                 id = query<COUNT>(geo, ray, t, first);
+#endif
             }
             bool done = false, lights = false;
             if (shadow) {                                       // :154-161
+                SPT_PROF(PB_SHADOW);
                 cnt.isectp++;
                 cnt.tests += first >= 0 ? (unsigned)(S.n - first) : (unsigned)S.n;
                 if (id < 0) {
-                    const float4 le = S.emi[S.lights[li]];
+                    const float4 le = S.lrec[3 * li + 2];
                     lsum = vadd(lsum, vsmul(lw, mk(le.x, le.y, le.z)));
                 }
                 li++;
@@ -378,6 +458,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 if (id < 0) {
                     done = true;
                 } else {
+                    SPT_PROF(PB_NEAREST);
                     const float4 og = S.geo[id], oe = S.emi[id], oc = S.col[id];
                     hit = vsmul(t, ray.d);
                     hit = vadd(ray.o, hit);
@@ -395,12 +476,14 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                         }
                         done = true;
                     } else if (refl == DIFF) {
+                        SPT_PROF(PB_DIFF);
                         specular = false;
                         thr = vmul(thr, mk(oc.x, oc.y, oc.z));
                         lsum = mk(0.f, 0.f, 0.f);
                         li = 0;
                         lights = true;
                     } else if (refl == SPEC) {
+                        SPT_PROF(PB_SPEC);
                         specular = true;
                         v3 nd = vsmul(2.f * vdot(normal, ray.d), normal);
                         nd = vsub(ray.d, nd);
@@ -408,13 +491,19 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                         ray.o = hit;
                         ray.d = nd;
                     } else {
+                        SPT_PROF(PB_REFR);
                         specular = true;
                         v3 nd = vsmul(2.f * vdot(normal, ray.d), normal);
                         nd = vsub(ray.d, nd);
-                        const bool into = vdot(normal, nl) > 0;
+                        // nl = inv_sign * normal with inv_sign = +-1, so (rounding
+                        // being sign-symmetric) vdot(normal, nl) = inv_sign * |n|^2
+                        // and vdot(ray.d, nl) = inv_sign * dp exactly: into is
+                        // dp <= 0 (false for NaN, as the reference's NaN dot) and
+                        // ddn is dp with inv_sign's sign.
+                        const bool into = dp <= 0.f;
                         const float nc = 1.f, nt = 1.5f;
                         const float nnt = into ? nc / nt : nt / nc;
-                        const float ddn = vdot(ray.d, nl);
+                        const float ddn = inv_sign * dp;
                         const float cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
                         if (cos2t < 0.f) {
                             thr = vmul(thr, mk(oc.x, oc.y, oc.z));
@@ -458,9 +547,9 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 // oracle does (:138).
                 shadow = false;
                 for (; li < S.nlights; li++) {
-                    const int i = S.lights[li];
-                    const float4 lc = S.col[i];                 // colour.xyz, rad
-                    const float4 lg = S.geo[i];                 // centre
+                    SPT_PROF(PB_LIGHT);
+                    const float4 lg = S.lrec[3 * li];           // centre
+                    const float4 lc = S.lrec[3 * li + 1];       // colour.xyz, rad
                     const float lrad = lc.w;
                     const float u2 = get_random(s0, s1);
                     const float u1 = get_random(s0, s1);
@@ -502,6 +591,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     if (DL) {
                         done = true;
                     } else {
+                        SPT_PROF(PB_BOUNCE);
                         const float r1 = 2.f * PI_F * get_random(s0, s1);
                         const float r2 = get_random(s0, s1);
                         const float r2s = sqrt_exact(r2);
@@ -522,6 +612,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 }
             }
             if (done) {                                         // :110-118 running average
+                SPT_PROF(PB_DONE);
                 const int current = first_sample + k;
                 if (current == 0) {
                     col = rad;
@@ -551,6 +642,28 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         const unsigned long long c[4] = {cnt.isect, cnt.isectp, cnt.tests, cnt.samples};
         flush_counters<4>(counters, c);
     }
+#ifdef RT_SPT_TRACE
+    {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        unsigned mx = tr_iters;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, off, 64));
+        const unsigned sum = (unsigned)wave_sum_u64(tr_iters);
+        const size_t wv = (size_t)blockIdx.x * (blockDim.x >> 6) + wave;
+        if (lane == 0 && g_spt_trace) {
+            g_spt_trace[2 * wv] = make_uint4((unsigned)tr_t0, (unsigned)t1, __builtin_amdgcn_s_getreg(0xF804),
+                                             __builtin_amdgcn_s_getreg(0xF814));
+            g_spt_trace[2 * wv + 1] = make_uint4(sum, mx, 0u, 0u);
+        }
+    }
+#endif
+#ifdef RT_SPT_PROF
+#pragma unroll
+    for (int b = 0; b < PB_N; b++) {
+        const unsigned long long l = wave_sum_u64(prof_l[b]), v = wave_sum_u64(prof_w[b]);
+        if (lane == 0) { atomicAdd(&g_spt_prof[2 * b], l); atomicAdd(&g_spt_prof[2 * b + 1], v); }
+    }
+#endif
 }
 
 }  // namespace smallpt
@@ -568,38 +681,53 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
 // staging, device SoA + light list for scenes above the LDS budget.
 struct spt_scene {
     int device = -1;
+    int cus = 256;
     int n = 0;
     rt_sphere *d_spheres = nullptr;   // n x 44 B
-    float4 *d_soa = nullptr;          // geo | emi | col (n each), then lights (int)
+    float4 *d_soa = nullptr;          // geo | emi | col (n each) | light records (3 per light)
     int nlights = 0;
     void *d_bvh = nullptr;            // nodes | geo | id | always geo | always id (large scenes)
     rt::smallpt::BvhView bvh = {};
     std::vector<rt_sphere> host;
+    bool force_global = false;        // RT_SPT_GEO=global: scalar-load path at any size (A/B)
 };
 
 namespace {
 
+// Launch shape: one wave per 8x8 tile of rows [r0, r1).  256-thread blocks
+// (several per CU, dispatched as CUs free up) unless the window has at most
+// four tiles per SIMD (a multi-GPU row band): then 1024-thread blocks with
+// more than half the CU's LDS reserved, so a CU holds exactly one and every
+// SIMD gets four waves, instead of the dispatcher's uneven 3..5 per SIMD.
+struct Shape { int tiles_x, ntiles, wpb, nblocks; };
+Shape launch_shape(const spt_scene &sc, int w, int r0, int r1)
+{
+    Shape g;
+    g.tiles_x = (w + 7) / 8;
+    g.ntiles = g.tiles_x * ((r1 - r0 + 7) / 8);
+    g.wpb = g.ntiles <= 16 * sc.cus ? 16 : 4;
+    if (const char *e = getenv("RT_SPT_WPB")) g.wpb = atoi(e) == 16 ? 16 : 4;   // A/B
+    g.nblocks = (g.ntiles + g.wpb - 1) / g.wpb;
+    return g;
+}
+
 template <bool DL, bool COUNT, int GEO>
-void launch(dim3 grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam, float *colors,
+void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &cam, float *colors,
             const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h, int r0, int r1,
             int first, int ns, unsigned long long *cnt)
 {
     constexpr bool LDS = GEO == rt::smallpt::GEO_LDS;
     const int n = sc.n;
-    const float4 *gg = nullptr, *ge = nullptr, *gc = nullptr;
-    const int *gl = nullptr;
-    if (!LDS) {
-        gg = sc.d_soa; ge = gg + n; gc = ge + n;
-        gl = (const int *)(gc + n);
-    }
-    const size_t lds = LDS ? (size_t)n * 3 * sizeof(float4) + (size_t)(n + 1) * sizeof(int) : 0;
-    hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO>), grid, dim3(256), lds, s,
-                       sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, gg, ge,
-                       gc, gl, sc.nlights, sc.bvh, cnt);
+    const float4 *gg = sc.d_soa, *ge = gg + n, *gc = ge + n, *gl = gc + n;
+    size_t lds = LDS ? (size_t)(3 * n + 3 * sc.nlights) * sizeof(float4) : 0;
+    if (g.wpb == 16 && lds < 81 * 1024) lds = 81 * 1024;   // > half the CU's 160 KiB: one block per CU
+    hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
+                       sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, first,
+                       ns, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt);
 }
 
 template <int GEO>
-void launch_mode(bool dl, bool count, dim3 grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam,
+void launch_mode(bool dl, bool count, const Shape &grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam,
                  float *colors, const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h,
                  int r0, int r1, int first, int ns, unsigned long long *cnt)
 {
@@ -844,11 +972,14 @@ extern "C" int spt_scene_create(const rt_sphere *spheres, unsigned nspheres, spt
     if (rc) return rc;
     spt_scene *sc = new spt_scene();
     sc->device = st->device;
+    if (st->cus > 0) sc->cus = st->cus;
     sc->n = (int)nspheres;
     sc->host.assign(spheres, spheres + nspheres);
+    const char *geo_env = getenv("RT_SPT_GEO");
+    sc->force_global = geo_env && !strcmp(geo_env, "global");
     const int n = sc->n;
-    std::vector<float4> soa((size_t)3 * n + (n + 3) / 4);
-    int *lights = (int *)(soa.data() + 3 * (size_t)n);
+    std::vector<float4> soa((size_t)3 * n);
+    std::vector<int> lights;
     for (int i = 0; i < n; i++) {
         const rt_sphere &q = spheres[i];
         soa[i] = make_float4(q.p.x, q.p.y, q.p.z, q.rad * q.rad);
@@ -857,7 +988,14 @@ extern "C" int spt_scene_create(const rt_sphere *spheres, unsigned nspheres, spt
         memcpy(&frefl, &refl, 4);
         soa[n + i] = make_float4(q.e.x, q.e.y, q.e.z, frefl);
         soa[2 * (size_t)n + i] = make_float4(q.c.x, q.c.y, q.c.z, q.rad);
-        if (!((q.e.x == 0.f) && (q.e.x == 0.f) && (q.e.z == 0.f))) lights[sc->nlights++] = i;  // vec.h:44
+        if (!((q.e.x == 0.f) && (q.e.x == 0.f) && (q.e.z == 0.f))) lights.push_back(i);  // vec.h:44
+    }
+    sc->nlights = (int)lights.size();
+    for (int i : lights) {                 // light records: geo, col, emi of each light, ascending
+        const float4 g = soa[i], c = soa[2 * (size_t)n + i], e = soa[(size_t)n + i];
+        soa.push_back(g);
+        soa.push_back(c);
+        soa.push_back(e);
     }
     hipError_t e = hipMalloc(&sc->d_spheres, sizeof(rt_sphere) * n);
     if (e == hipSuccess) e = hipMalloc(&sc->d_soa, sizeof(float4) * soa.size());
@@ -899,7 +1037,7 @@ extern "C" int spt_scene_render_async(const spt_scene *sc, const rt_camera *came
                                row_end, first_sample, nsamples, mode);
     if (rc) return rc;
     if (row_begin == row_end) return RT_OK;
-    dim3 grid((w + 15) / 16, (row_end - row_begin + 15) / 16);
+    const Shape grid = launch_shape(*sc, w, row_begin, row_end);
     hipStream_t s = (hipStream_t)stream;
     unsigned long long *cnt = (unsigned long long *)d_counters;
     const bool dl = mode == SPT_DIRECT_LIGHTING;
@@ -907,7 +1045,8 @@ extern "C" int spt_scene_render_async(const spt_scene *sc, const rt_camera *came
         launch_mode<rt::smallpt::GEO_BVH>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in,
                                           d_seeds_out, d_pixels, w, h, row_begin, row_end, first_sample,
                                           nsamples, cnt);
-    else if (sc->n <= rt::smallpt::MAXS_LDS)
+    else if ((size_t)(3 * sc->n + 3 * sc->nlights) * sizeof(float4) <= (size_t)rt::smallpt::MAX_LDS_BYTES &&
+             !sc->force_global)
         launch_mode<rt::smallpt::GEO_LDS>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
                              d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
     else
@@ -945,6 +1084,27 @@ extern "C" int spt_render_async(const rt_sphere *d_spheres, unsigned nspheres, c
     spt_scene_destroy(sc);
     return rc;
 }
+
+#ifdef RT_SPT_PROF
+// Tools-only: reads and clears the block profile (18 counters).
+extern "C" int spt_prof_read(unsigned long long *out)
+{
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(rt::smallpt::g_spt_prof), sizeof(rt::smallpt::g_spt_prof));
+    static const unsigned long long zero[2 * rt::smallpt::PB_N] = {};
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(rt::smallpt::g_spt_prof), zero, sizeof(zero));
+    return e == hipSuccess ? RT_OK : rtrt::fail_hip(e, "spt_prof_read");
+}
+#endif
+
+#ifdef RT_SPT_TRACE
+// Tools-only: sets the wave-timeline buffer (uint4 per wave of the grid; null: off).
+extern "C" int spt_trace_set(void *buf)
+{
+    uint4 *p = (uint4 *)buf;
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(rt::smallpt::g_spt_trace), &p, sizeof(p));
+    return e == hipSuccess ? RT_OK : rtrt::fail_hip(e, "spt_trace_set");
+}
+#endif
 
 extern "C" int spt_render(const rt_sphere *spheres, unsigned nspheres, const rt_camera *camera,
                           float *colors, uint32_t *seeds, uint32_t *pixels, int w, int h,

@@ -3,7 +3,8 @@ process per variant, interleaved rounds, HIP-event time on the launch stream).
 
     KERNEL=smallpt|whitted LIBS=a,b ROUNDS=2 REPS=5 python tools/ab.py
 
-smallpt: Cornell 1920x1080, SPP (default 64) samples per launch.
+smallpt: Cornell 1920x1080, SPP (default 64) samples per launch; BAND=k/N renders
+only row band k of N (rtamd.dist.row_band: the per-GPU work of an N-GPU frame).
 whitted: raytracer3.0.06 scene, 1920x1080, rows [20, H-70).
 """
 import ctypes as C
@@ -35,6 +36,11 @@ def child():
                                            st.cuda_stream))
     else:
         SPP = int(os.environ.get("SPP", "64"))
+        r0, r1 = 0, H
+        if os.environ.get("BAND"):
+            from rtamd import dist as rdist
+            k, N = (int(v) for v in os.environ["BAND"].split("/"))
+            r0, r1 = rdist.row_band(k, N, H)
         S, n = rtamd.scenes.cornell()
         cam = rtamd.scenes.cornell_camera(W, H)
         sc = rtamd.SmallptScene(S, n)
@@ -45,7 +51,7 @@ def child():
 
         def run():
             rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
-                                                 seeds.data_ptr(), px.data_ptr(), W, H, 0, H, 0, SPP, 0,
+                                                 seeds.data_ptr(), px.data_ptr(), W, H, r0, r1, 0, SPP, 0,
                                                  None, st.cuda_stream))
     run()
     torch.cuda.synchronize()
@@ -64,8 +70,9 @@ def child():
         for b, nm in enumerate(names):
             lanes, waves = buf[2 * b], buf[2 * b + 1]
             print("  %-8s lanes %14d waves %12d lanes/wave-exec %.1f" % (nm, lanes, waves, lanes / max(waves, 1)))
-    print("%s %s min %.3f med %.3f ms" % (os.environ.get("KERNEL", "smallpt"), os.environ.get("VARIANT", "?"),
-                                         min(ts), float(np.median(ts))), flush=True)
+    print("%s %s %s min %.3f med %.3f ms" % (os.environ.get("KERNEL", "smallpt"), os.environ.get("BAND", ""),
+                                            os.environ.get("VARIANT", "?"), min(ts), float(np.median(ts))),
+          flush=True)
 
 
 def main():
