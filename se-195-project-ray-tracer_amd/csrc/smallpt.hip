@@ -388,42 +388,75 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         // Per-lane path state.  Every loop iteration issues exactly ONE ray
         // query for every live lane -- the path ray (nearest hit) or, while a
         // DIFF vertex is sampling its lights, that light's shadow ray (any hit)
-        // -- so the sphere loop, which is most of the work, runs with all lanes
-        // of the wave active instead of the shadow tests running as a second
-        // loop under the DIFF branch.  Per lane the operations and RNG draws
-        // are the reference's, in its order.
+        // -- so the sphere loop runs with all lanes of the wave active.  The
+        // shading after it is organised by the operations it needs rather than
+        // by material, so that lanes in different situations share one pass of
+        // the expensive code (RNG draws, square root, sincos, normalisation,
+        // division) instead of each situation running its own divergent block:
+        //   * pass A builds a light sample's shadow ray (SampleLights) or a
+        //     REFR hit's Fresnel-chosen ray;
+        //   * pass B builds a DIFF bounce ray or the next sample's camera ray.
+        // A lane that needs both in one iteration (a light sample that yields
+        // no shadow ray, then the bounce; a refraction that ends the path,
+        // then the camera ray) runs A before B, so per lane the operations and
+        // RNG draws are the reference's, in its order.
         ray3 ray;              // the ray queried next
-        v3 rad, thr;
-        int depth;
-        bool specular;
+        v3 rad = mk(0.f, 0.f, 0.f), thr = mk(1.f, 1.f, 1.f);
+        int depth = 0;
+        bool specular = true;
         bool shadow = false;   // ray is the shadow ray of light li
-        v3 hit, nl;            // the DIFF vertex (SampleLights' hitPoint, normal)
+        v3 hit, nl;            // the last hit point and its oriented normal (SampleLights' args)
         v3 lsum;               // SampleLights' running result
         float lmax = 0.f;      // shadow ray maxt (len - EPSILON)
         float lw = 0.f;        // that light's weight s (geomfunc.h:159)
         int li = 0;
-        // :89-105 camera ray; run by the lane that starts a sample, right after
-        // finishing the previous one (one branch for both).
-        const auto camera_ray = [&]() {
-            const float r1 = get_random(s0, s1) - .5f;
-            const float r2 = get_random(s0, s1) - .5f;
-            const float kcx = (x + r1) * invW - .5f;
-            const float kcy = (y + r2) * invH - .5f;
-            v3 rdir = mk(cam.x.x * kcx + cam.y.x * kcy + cam.dir.x,
-                         cam.x.y * kcx + cam.y.y * kcy + cam.dir.y,
-                         cam.x.z * kcx + cam.y.z * kcy + cam.dir.z);
-            v3 rorig = vsmul(0.1f, rdir);
-            rorig = vadd(rorig, mk(cam.orig.x, cam.orig.y, cam.orig.z));
-            rdir = vnorm(rdir);
-            ray.o = rorig; ray.d = rdir;
-            rad = mk(0.f, 0.f, 0.f);
-            thr = mk(1.f, 1.f, 1.f);
-            depth = 0;
-            specular = true;
-        };
         int k = 0;
-        if (nsamples > 0) camera_ray();
-        while (k < nsamples) {
+        bool need_cam = nsamples > 0, need_bounce = false;
+        constexpr float nc = 1.f, nt = 1.5f;
+        while (true) {
+            // ---- pass B: DIFF bounce (geomfunc.h:229-269) or camera ray
+            // (smallptCPU.cpp:89-105).  Both draw two randoms and normalise
+            // one vector.
+            if (need_bounce || need_cam) {
+                SPT_PROF(PB_BOUNCE);
+                const float x1 = get_random(s0, s1);
+                const float x2 = get_random(s0, s1);
+                // bounce: r1 = 2 PI x1, r2 = x2, u = norm(a x w)
+                const v3 wv = nl;
+                const v3 a = (fabsf(wv.x) > .1f) ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
+                const v3 cu = vxcross(a, wv);
+                // camera: r1 = x1 - .5, r2 = x2 - .5
+                const float kcx = (x + (x1 - .5f)) * invW - .5f;
+                const float kcy = (y + (x2 - .5f)) * invH - .5f;
+                const v3 rdir = mk(cam.x.x * kcx + cam.y.x * kcy + cam.dir.x,
+                                   cam.x.y * kcx + cam.y.y * kcy + cam.dir.y,
+                                   cam.x.z * kcx + cam.y.z * kcy + cam.dir.z);
+                const v3 vn = vnorm(need_bounce ? cu : rdir);
+                if (need_bounce) {
+                    const float r1 = 2.f * PI_F * x1;
+                    const float r2s = sqrt_exact(x2);
+                    const v3 v = vxcross(wv, vn);
+                    float sn1, cs1;
+                    rtm::sincosf(r1, sn1, cs1);
+                    const v3 u = vsmul(cs1 * r2s, vn);
+                    v3 nd = vadd(u, vsmul(sn1 * r2s, v));
+                    nd = vadd(nd, vsmul(sqrt_exact(1 - x2), wv));
+                    ray.o = hit;
+                    ray.d = nd;
+                } else {
+                    v3 rorig = vsmul(0.1f, rdir);
+                    rorig = vadd(rorig, mk(cam.orig.x, cam.orig.y, cam.orig.z));
+                    ray.o = rorig;
+                    ray.d = vn;
+                    rad = mk(0.f, 0.f, 0.f);
+                    thr = mk(1.f, 1.f, 1.f);
+                    depth = 0;
+                    specular = true;
+                }
+                need_bounce = need_cam = false;
+            }
+            if (k >= nsamples) break;
+
             SPT_PROF(PB_ITER);
 #ifdef RT_SPT_TRACE
             tr_iters++;
@@ -441,7 +474,10 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 id = query<COUNT>(geo, ray, t, first);
 #endif
             }
-            bool done = false, lights = false;
+            bool done = false, lights = false, a_R = false;
+            v3 normal, nd;                 // REFR: the hit's normal and reflected direction
+            float dp = 0.f, inv_sign = 1.f;
+            float4 oc = make_float4(0.f, 0.f, 0.f, 0.f);
             if (shadow) {                                       // :154-161
                 SPT_PROF(PB_SHADOW);
                 cnt.isectp++;
@@ -452,6 +488,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 }
                 li++;
                 lights = true;
+                shadow = false;
             } else {                                            // one bounce of :182-337
                 cnt.isect++;
                 cnt.tests += S.n;
@@ -459,13 +496,14 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     done = true;
                 } else {
                     SPT_PROF(PB_NEAREST);
-                    const float4 og = S.geo[id], oe = S.emi[id], oc = S.col[id];
+                    const float4 og = S.geo[id], oe = S.emi[id];
+                    oc = S.col[id];
                     hit = vsmul(t, ray.d);
                     hit = vadd(ray.o, hit);
-                    v3 normal = vsub(hit, mk(og.x, og.y, og.z));
+                    normal = vsub(hit, mk(og.x, og.y, og.z));
                     normal = vnorm(normal);
-                    const float dp = vdot(normal, ray.d);
-                    const float inv_sign = -1.f * (dp > 0 ? 1.f : -1.f);
+                    dp = vdot(normal, ray.d);
+                    inv_sign = -1.f * (dp > 0 ? 1.f : -1.f);
                     nl = vsmul(inv_sign, normal);
                     const int refl = __float_as_int(oe.w);
                     if (!((oe.x == 0.f) && (oe.x == 0.f) && (oe.z == 0.f))) {
@@ -482,89 +520,75 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                         lsum = mk(0.f, 0.f, 0.f);
                         li = 0;
                         lights = true;
-                    } else if (refl == SPEC) {
-                        SPT_PROF(PB_SPEC);
-                        specular = true;
-                        v3 nd = vsmul(2.f * vdot(normal, ray.d), normal);
-                        nd = vsub(ray.d, nd);
-                        thr = vmul(thr, mk(oc.x, oc.y, oc.z));
-                        ray.o = hit;
-                        ray.d = nd;
                     } else {
-                        SPT_PROF(PB_REFR);
                         specular = true;
-                        v3 nd = vsmul(2.f * vdot(normal, ray.d), normal);
+                        nd = vsmul(2.f * vdot(normal, ray.d), normal);
                         nd = vsub(ray.d, nd);
-                        // nl = inv_sign * normal with inv_sign = +-1, so (rounding
-                        // being sign-symmetric) vdot(normal, nl) = inv_sign * |n|^2
-                        // and vdot(ray.d, nl) = inv_sign * dp exactly: into is
-                        // dp <= 0 (false for NaN, as the reference's NaN dot) and
-                        // ddn is dp with inv_sign's sign.
-                        const bool into = dp <= 0.f;
-                        const float nc = 1.f, nt = 1.5f;
-                        const float nnt = into ? nc / nt : nt / nc;
-                        const float ddn = inv_sign * dp;
-                        const float cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
-                        if (cos2t < 0.f) {
+                        if (refl == SPEC) {
+                            SPT_PROF(PB_SPEC);
                             thr = vmul(thr, mk(oc.x, oc.y, oc.z));
                             ray.o = hit;
                             ray.d = nd;
                         } else {
-                            const float kk = (into ? 1.f : -1.f) * (ddn * nnt + sqrt_exact(cos2t));
-                            const v3 nkk = vsmul(kk, normal);
-                            v3 td = vsmul(nnt, ray.d);
-                            td = vsub(td, nkk);
-                            td = vnorm(td);
-                            const float a = nt - nc, b = nt + nc;
-                            const float R0 = a * a / (b * b);
-                            const float c = 1 - (into ? -ddn : vdot(td, normal));
-                            const float Re = R0 + (1 - R0) * c * c * c * c * c;
-                            const float Tr = 1.f - Re;
-                            const float P = .25f + .5f * Re;
-                            const float RP = Re / P;
-                            const float TP = Tr / (1.f - P);
-                            if (get_random(s0, s1) < P) {
-                                thr = vsmul(RP, thr);
-                                thr = vmul(thr, mk(oc.x, oc.y, oc.z));
-                                ray.o = hit;
-                                ray.d = nd;
-                            } else {
-                                thr = vsmul(TP, thr);
-                                thr = vmul(thr, mk(oc.x, oc.y, oc.z));
-                                ray.o = hit;
-                                ray.d = td;
-                            }
+                            SPT_PROF(PB_REFR);
+                            a_R = true;
                         }
                     }
                     depth++;
-                    done = done || (!lights && depth > 6);      // :184 at the next bounce
+                    done = done || (!lights && !a_R && depth > 6);   // :184 at the next bounce
                 }
             }
-            if (lights) {
-                // SampleLights (:112-165) from light li on: stop at the next
-                // light that needs a shadow test; UniformSampleSphere's two
-                // GetRandom() arguments are drawn second-first, as the g++-built
-                // oracle does (:138).
-                shadow = false;
-                for (; li < S.nlights; li++) {
+
+            // ---- pass A: SampleLights (:112-165) from light li on, stopping at
+            // the next light that needs a shadow test, and/or the REFR branch
+            // (:281-336).  Repeats only while some lane skips a light (several
+            // lights).  UniformSampleSphere's two GetRandom() arguments are
+            // drawn second-first, as the g++-built oracle does (:138); the
+            // Russian-roulette draw of REFR is taken before its Fresnel terms
+            // (no other draw of the lane lies between).
+            bool a_L = lights && li < S.nlights;
+            bool lights_done = lights && !a_L;
+            const bool was_R = a_R;
+            // nl = inv_sign * normal with inv_sign = +-1, so (rounding being
+            // sign-symmetric) vdot(normal, nl) = inv_sign * |n|^2 and
+            // vdot(ray.d, nl) = inv_sign * dp exactly: into is dp <= 0 (false
+            // for NaN, as the reference's NaN dot) and ddn is dp signed.
+            const bool into = dp <= 0.f;
+            const float nnt = into ? nc / nt : nt / nc;
+            const float ddn = inv_sign * dp;
+            const float cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
+            const bool tir = cos2t < 0.f;
+            // One pass for every lane that needs A, then further light-only
+            // passes while some lane skipped a light (scenes with several
+            // lights).  The body is one lambda instantiated twice so the
+            // common single pass is straight-line code (a loop around both
+            // made the compiler shuffle all loop-carried state every pass).
+            const auto pass_a = [&](const bool with_r) {
+                {
                     SPT_PROF(PB_LIGHT);
-                    const float4 lg = S.lrec[3 * li];           // centre
-                    const float4 lc = S.lrec[3 * li + 1];       // colour.xyz, rad
-                    const float lrad = lc.w;
-                    const float u2 = get_random(s0, s1);
-                    const float u1 = get_random(s0, s1);
-                    const float zz = 1.f - 2.f * u1;            // UniformSampleSphere, :61-69
+                    float4 lg = make_float4(0.f, 0.f, 0.f, 0.f), lc = lg;
+                    if (a_L) {
+                        lg = S.lrec[3 * li];                    // centre
+                        lc = S.lrec[3 * li + 1];                // colour.xyz, rad
+                    }
+                    float x1 = 0.f, x2 = 0.f;
+                    if (a_L || (with_r && !tir)) x1 = get_random(s0, s1);   // L: u2; R: the roulette draw
+                    if (a_L) x2 = get_random(s0, s1);           // L: u1
+                    const float zz = 1.f - 2.f * x2;            // UniformSampleSphere, :61-69
                     const float q = 1.f - zz * zz;
-                    const float rr = sqrt_exact((0.f > q) ? 0.f : q);
-                    const float phi = 2.f * PI_F * u2;
+                    const float sq = sqrt_exact((!with_r || a_L) ? ((0.f > q) ? 0.f : q) : (tir ? 1.f : cos2t));
+                    const float phi = 2.f * PI_F * x1;
                     float sp_sin, sp_cos;
                     rtm::sincosf(phi, sp_sin, sp_cos);
-                    const v3 unit = mk(rr * sp_cos, rr * sp_sin, zz);
-                    v3 sp = vsmul(lrad, unit);
+                    const v3 unit = mk(sq * sp_cos, sq * sp_sin, zz);
+                    v3 sp = vsmul(lc.w, unit);
                     sp = vadd(sp, mk(lg.x, lg.y, lg.z));
-                    v3 sd = vsub(sp, hit);
-                    const float dd = vdot(sd, sd);
-                    float len, ilen;
+                    const v3 vl = vsub(sp, hit);                // shadow ray direction
+                    const float kk = (into ? 1.f : -1.f) * (ddn * nnt + sq);
+                    const v3 vr = vsub(vsmul(nnt, ray.d), vsmul(kk, normal));   // refracted direction
+                    const v3 vv = (!with_r || a_L) ? vl : vr;
+                    const float dd = vdot(vv, vv);
+                    float len, ilen;                            // sqrtf(dd), 1.f / len
                     if (!wave_any(!sqrt_nr_ok(dd))) {
                         len = sqrt_nr(dd);
                         ilen = rcp_nr(len);
@@ -572,43 +596,65 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                         len = sqrt_rn(dd);
                         ilen = 1.f / len;
                     }
-                    sd = vsmul(ilen, sd);
-                    float wo = vdot(sd, unit);
-                    if (wo > 0.f) continue;
-                    wo = -wo;
-                    const float wi = vdot(sd, nl);
-                    if (wi > 0.f) {
+                    const v3 vn = vsmul(ilen, vv);
+                    const float dv = vdot(vn, (!with_r || a_L) ? unit : normal);   // L: wo; R: vdot(td, normal)
+                    // L: weight (4 PI rad^2) wi wo / len^2; R: RP = Re / P or TP = Tr / (1 - P)
+                    const float wo = -dv;
+                    const float wi = vdot(vn, nl);
+                    const bool lit = a_L && !(dv > 0.f) && wi > 0.f;
+                    const float a = nt - nc, b = nt + nc;
+                    const float R0 = a * a / (b * b);
+                    const float c = 1 - (into ? -ddn : dv);
+                    const float Re = R0 + (1 - R0) * c * c * c * c * c;
+                    const float Tr = 1.f - Re;
+                    const float P = .25f + .5f * Re;
+                    const bool refl_pick = x1 < P;
+                    const bool l_lane = !with_r || a_L;
+                    const float num = l_lane ? (4.f * PI_F * lc.w * lc.w) * wi * wo : (refl_pick ? Re : Tr);
+                    const float den = l_lane ? len * len : (refl_pick ? P : 1.f - P);
+                    const float quo = num / den;
+                    if (!with_r || a_L) {
+                        if (lit) {
+                            ray.o = hit;
+                            ray.d = vn;
+                            lmax = len - EPS;
+                            lw = quo;
+                            shadow = true;
+                            a_L = false;
+                        } else {
+                            li++;
+                            a_L = li < S.nlights;
+                            lights_done = !a_L;
+                        }
+                    } else {
                         ray.o = hit;
-                        ray.d = sd;
-                        lmax = len - EPS;
-                        lw = (4.f * PI_F * lrad * lrad) * wi * wo / (len * len);
-                        shadow = true;
-                        break;
+                        if (tir) {
+                            thr = vmul(thr, mk(oc.x, oc.y, oc.z));
+                            ray.d = nd;
+                        } else {
+                            thr = vsmul(quo, thr);
+                            thr = vmul(thr, mk(oc.x, oc.y, oc.z));
+                            ray.d = refl_pick ? nd : vn;
+                        }
+                        a_R = false;
                     }
                 }
-                if (!shadow) {                                  // :229-269
-                    rad = vadd(rad, vmul(thr, lsum));
-                    if (DL) {
-                        done = true;
-                    } else {
-                        SPT_PROF(PB_BOUNCE);
-                        const float r1 = 2.f * PI_F * get_random(s0, s1);
-                        const float r2 = get_random(s0, s1);
-                        const float r2s = sqrt_exact(r2);
-                        const v3 wv = nl;
-                        const v3 a = (fabsf(wv.x) > .1f) ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
-                        v3 u = vnorm(vxcross(a, wv));
-                        v3 v = vxcross(wv, u);
-                        float sn1, cs1;
-                        rtm::sincosf(r1, sn1, cs1);
-                        u = vsmul(cs1 * r2s, u);
-                        v = vsmul(sn1 * r2s, v);
-                        v3 nd = vadd(u, v);
-                        nd = vadd(nd, vsmul(sqrt_exact(1 - r2), wv));
-                        ray.o = hit;
-                        ray.d = nd;
-                        done = depth > 6;
-                    }
+            };
+            if (a_L || a_R) pass_a(true);
+            while (wave_any(a_L)) {
+                if (a_L) pass_a(false);
+            }
+            if (was_R) done = depth > 6;
+            if (lights_done) {                                  // :229-230, then the bounce
+                rad = vadd(rad, vmul(thr, lsum));
+                if (DL) {
+                    done = true;                                // :413-414
+                } else if (depth > 6) {                         // the bounce's two draws, then :184
+                    (void)get_random(s0, s1);
+                    (void)get_random(s0, s1);
+                    done = true;
+                } else {
+                    need_bounce = true;
                 }
             }
             if (done) {                                         // :110-118 running average
@@ -625,7 +671,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 }
                 cnt.samples++;
                 k++;
-                if (k < nsamples) camera_ray();
+                need_cam = k < nsamples;
             }
         }
         if (nsamples > 0) {
