@@ -9,7 +9,9 @@ running average, toInt pack -- plus, for N > 1, the RCCL all-gather that
 assembles the HDR accumulator and the RGBA8 frame on every rank.
 
 Rows are sharded over ranks in equal contiguous bands (strong scaling: the
-frame is fixed, each of N GPUs renders 1/N of it).  Rays = Intersect +
+frame is fixed, each of N GPUs renders 1/N of it); for N > 1 one in-place
+RCCL all-gather of the HDR accumulator per frame, then every rank repacks the
+RGBA8 frame from it (spt_pack_pixels_async).  Rays = Intersect +
 IntersectP calls, counted by the kernel itself.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-whitted]
@@ -228,7 +230,10 @@ def main():
     r0, r1 = rdist.row_band(rank, world, H)
     B = r1 - r0
     s = torch.cuda.current_stream(dev)
-    gather = rdist.FrameGather(colors, pixels, rank, world, W, H)
+    def pack():                  # RGBA8 frame from the gathered HDR accumulator (toInt, bit-exact)
+        rtamd.check(L.spt_pack_pixels_async(colors.data_ptr(), pixels.data_ptr(), W, H, 0, H, s.cuda_stream))
+
+    gather = rdist.FrameGather(colors, pixels, rank, world, W, H, pack=pack)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
 
@@ -242,7 +247,7 @@ def main():
                                        s.cuda_stream))
         if i is not None:
             ev[i][1].record(s)
-        gather.gather()          # RCCL all-gather of the HDR + RGBA8 bands (no-op at N=1)
+        gather.gather()          # RCCL all-gather of the HDR bands + RGBA8 repack (no-op at N=1)
 
     for _ in range(args.warmup):
         step()
@@ -295,7 +300,7 @@ def main():
         "data": "synthetic: reference Cornell scene (scene.h:29-40), glibc rand() seeds, random-free camera",
         "config": {"workload": "smallpt Cornell 1920x1080 64spp RadiancePathTracing, one frame per step",
                    "frame": [W, H], "spp": SPP, "spheres": ns, "rows_per_gpu": B,
-                   "parallelism": "row bands x%d + RCCL all-gather" % world if world > 1 else "single GPU"},
+                   "parallelism": "row bands x%d + RCCL HDR all-gather" % world if world > 1 else "single GPU"},
         "frames_per_s": round(1e3 / ms_per_step, 3),
         "Msamples_per_s": round(W * H * SPP / (ms_per_step * 1e-3) / 1e6, 2),
         "rays_per_frame": rays_per_frame,

@@ -131,9 +131,9 @@ int spt_render_async(const rt_sphere *d_spheres, unsigned nspheres, const rt_cam
                      int first_sample, int nsamples, int mode, uint64_t *d_counters,
                      void *stream);
 
-/* Prepared scene: uploads the sphere array once (device AoS + SoA + light
- * list) and keeps the kernel-argument copy of the geometry that the
- * size-specialised kernels hold in SGPRs.  Reuse it across frames. */
+/* Prepared scene: uploads the sphere array once (device SoA of geometry,
+ * materials and per-light records; for >= 256 spheres also the exact-culling
+ * sphere hierarchy).  Reuse it across frames. */
 typedef struct spt_scene spt_scene;
 int spt_scene_create(const rt_sphere *spheres, unsigned nspheres, spt_scene **out);
 int spt_scene_destroy(spt_scene *scene);
@@ -143,6 +143,14 @@ int spt_scene_render_async(const spt_scene *scene, const rt_camera *camera, floa
                            const uint32_t *d_seeds_in, uint32_t *d_seeds_out, uint32_t *d_pixels,
                            int w, int h, int row_begin, int row_end, int first_sample, int nsamples,
                            int mode, uint64_t *d_counters, void *stream);
+
+/* The toInt pack of UpdateRenderingCPU (smallptCPU.cpp:120-122, vec.h:62)
+ * alone: d_pixels[y*w+x] for rows [row_begin,row_end) from the accumulator
+ * slots (h-y-1)*w+x of d_colors -- the pixels a render call writes, rebuilt
+ * from colours that arrived from other ranks (a row-band frame assembled by
+ * one colour all-gather).  Asynchronous on `stream`. */
+int spt_pack_pixels_async(const float *d_colors, uint32_t *d_pixels, int w, int h, int row_begin,
+                          int row_end, void *stream);
 
 /* Host helper: AllocateBuffers' seed fill (smallptGPU.cpp:105-110) --
  * srand(seed); seeds[i] = max(rand(), 2) for i < n, with the host libc's

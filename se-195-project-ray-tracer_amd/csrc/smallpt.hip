@@ -712,6 +712,21 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
 #endif
 }
 
+// toInt pack of rows [row_begin, row_end) from the accumulator: the pixels
+// render_kernel writes at the end of a launch (smallptCPU.cpp:120-122), for a
+// frame whose colour bands came from other ranks.
+__global__ void __launch_bounds__(256) pack_kernel(const float *__restrict__ colors, uint32_t *__restrict__ pixels,
+                                                   int w, int h, int row_begin, int row_end)
+{
+    const size_t n = (size_t)(row_end - row_begin) * w;
+    for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+        const int y = row_begin + (int)(p / w), x = (int)(p % w);
+        const size_t i = (size_t)(h - y - 1) * w + x;
+        pixels[(size_t)y * w + x] =
+            (uint32_t)(to_int(colors[3 * i]) | (to_int(colors[3 * i + 1]) << 8) | (to_int(colors[3 * i + 2]) << 16));
+    }
+}
+
 }  // namespace smallpt
 }  // namespace rt
 
@@ -1129,6 +1144,19 @@ extern "C" int spt_render_async(const rt_sphere *d_spheres, unsigned nspheres, c
     }
     spt_scene_destroy(sc);
     return rc;
+}
+
+extern "C" int spt_pack_pixels_async(const float *d_colors, uint32_t *d_pixels, int w, int h, int row_begin,
+                                     int row_end, void *stream)
+{
+    if (!d_colors || !d_pixels || w < 1 || h < 1 || row_begin < 0 || row_end > h || row_begin > row_end)
+        return rtrt::fail(RT_ERR_INVALID, "spt_pack_pixels_async: bad arguments");
+    const size_t n = (size_t)(row_end - row_begin) * w;
+    if (n == 0) return RT_OK;
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(rt::smallpt::pack_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_colors, d_pixels,
+                       w, h, row_begin, row_end);
+    return rtrt::check_launch("spt pack_kernel");
 }
 
 #ifdef RT_SPT_PROF

@@ -2,16 +2,20 @@
 
 SURVEY.md §8(e): every pixel is independent (own RNG words, own accumulator),
 so a frame splits into row bands with no data-path exchange; the only
-collective is the assembly of the HDR accumulator (12 B/px) and the RGBA8
-frame (4 B/px) on every rank -- two all-gathers per frame (RCCL over xGMI
-with backend "nccl", gloo on CPU for tests).  Splitting samples of a pixel
-over GPUs is NOT done: it would break the per-pixel RNG chain and the
-running-average order the parity contract pins.
+collective assembles the frame on every rank after a render call.  Splitting
+samples of a pixel over GPUs is NOT done: it would break the per-pixel RNG
+chain and the running-average order the parity contract pins.
 
 Band layout: rank k owns the k-th contiguous chunk of the FLIPPED colour /
 seed slots ((h-y-1)*w + x, smallptCPU.cpp:86), i.e. pixel rows
-[h-(k+1)B, h-kB) with B = h/world, so its colour band is one contiguous
-all-gather piece in rank order and its pixel band is contiguous too.
+[h-(k+1)B, h-kB) with B = h/world.  Its HDR band is then chunk k, in rank
+order, of the colour buffer, so the whole accumulator is assembled by ONE
+in-place all-gather (RCCL over xGMI with backend "nccl", gloo on CPU).  The
+RGBA8 frame is not sent at all: every rank rebuilds it from the gathered
+colours with the same toInt pack the kernel ends with (pack callback:
+spt_pack_pixels_async on the GPU), bit-identical to the bands the other ranks
+wrote.  Without a pack callback (CPU tests) the pixel bands are all-gathered
+too.
 """
 import torch
 import torch.distributed as dist
@@ -27,24 +31,26 @@ def row_band(rank, world, h):
 
 
 class FrameGather:
-    """Views of a full-frame colors (float32[3*w*h]) / pixels (int32[w*h])
-    pair for in-place all-gather of the per-rank bands."""
+    """Assembles a full frame -- colors (float32[3*w*h]) and pixels
+    (int32[w*h]) -- on every rank from the per-rank row bands."""
 
-    def __init__(self, colors, pixels, rank, world, w, h):
+    def __init__(self, colors, pixels, rank, world, w, h, pack=None):
         self.rank, self.world, self.w, self.h = rank, world, w, h
+        self.colors, self.pixels, self.pack = colors, pixels, pack
         B = h // world
-        self.col_parts = list(colors.view(world, 3 * B * w).unbind(0))
+        self.my_col = colors.view(world, 3 * B * w)[rank]
         self.px_parts = [pixels[(h - (k + 1) * B) * w:(h - k * B) * w] for k in range(world)]
-        self.my_col = self.col_parts[rank]
         self.my_px = self.px_parts[rank]
 
     def gather(self, group=None):
-        """Every rank ends with the whole frame.  The own band is passed as a
-        copy (the output list aliases it)."""
+        """Every rank ends with the whole frame."""
         if self.world == 1:
             return
-        dist.all_gather(self.col_parts, self.my_col.clone(), group=group)
-        dist.all_gather(self.px_parts, self.my_px.clone(), group=group)
+        dist.all_gather_into_tensor(self.colors, self.my_col.clone(), group=group)
+        if self.pack is not None:
+            self.pack()
+        else:
+            dist.all_gather(self.px_parts, self.my_px.clone(), group=group)
 
 
 def gather_seeds(seeds, rank, world, w, h, group=None):
@@ -53,5 +59,4 @@ def gather_seeds(seeds, rank, world, w, h, group=None):
     if world == 1:
         return
     B = h // world
-    parts = list(seeds.view(world, 2 * B * w).unbind(0))
-    dist.all_gather(parts, parts[rank].clone(), group=group)
+    dist.all_gather_into_tensor(seeds, seeds.view(world, 2 * B * w)[rank].clone(), group=group)

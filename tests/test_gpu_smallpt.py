@@ -234,3 +234,24 @@ def test_random_scenes_vs_oracle(rt, oracle, seed):
         g.render(k, counters=False)
     assert (g.colors.view(np.uint32) == f.colors.view(np.uint32)).all()
     assert (g.seeds == f.seeds).all() and (g.pixels == f.pixels).all()
+
+
+def test_pack_pixels_matches_render(rt):
+    """spt_pack_pixels_async (the repack after a multi-GPU colour all-gather)
+    rebuilds exactly the pixels the render kernel wrote, for a row window."""
+    import torch
+    w, h = 320, 200
+    f = rt.SmallptFrame(w, h)
+    f.render(3)
+    dev = torch.device("cuda", 0)
+    col = torch.from_numpy(f.colors).to(dev)
+    px = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    rt.check(rt.lib().spt_pack_pixels_async(col.data_ptr(), px.data_ptr(), w, h, 0, h, st))
+    torch.cuda.synchronize()
+    assert (px.cpu().numpy().view(np.uint32) == f.pixels).all()
+    px.zero_()
+    rt.check(rt.lib().spt_pack_pixels_async(col.data_ptr(), px.data_ptr(), w, h, 50, 120, st))
+    torch.cuda.synchronize()
+    got = px.cpu().numpy().view(np.uint32).reshape(h, w)
+    assert (got[50:120] == f.pixels.reshape(h, w)[50:120]).all() and not got[:50].any() and not got[120:].any()
