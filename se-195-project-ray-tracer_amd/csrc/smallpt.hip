@@ -361,11 +361,13 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     S.n = nspheres;
     const DynGeo geo{S.geo, S.n};
 
-    // 8x8 pixel tiles of the row window, one per wave; wave j of block b
-    // takes tile j * gridDim.x + b, so a block's waves sample the whole
-    // window (per-block, hence per-CU, work evens out).
+    // 8x8 pixel tiles of the row window, one per wave, in groups of four
+    // side by side (a 32x8 strip: whole 128-B lines of the seed, colour and
+    // pixel rows, so no line is fetched by two XCDs); group j of block b is
+    // j * gridDim.x + b, so the groups of a 16-wave block sample the whole
+    // window (per-CU work evens out when one block fills a CU).
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int tile = wave * (int)gridDim.x + (int)blockIdx.x;
+    const int tile = ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) * 4 + (wave & 3);
     const int x = (tile % tiles_x) * 8 + (lane & 7);
     const int y = row_begin + (tile / tiles_x) * 8 + (lane >> 3);
     const bool active = tile < ntiles && x < w && y < row_end;

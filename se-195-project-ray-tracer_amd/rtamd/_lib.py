@@ -78,7 +78,8 @@ def lib():
     L.spt_scene_create.argtypes = [vp, u, C.POINTER(vp)]
     L.spt_scene_destroy.argtypes = [vp]
     L.spt_scene_render_async.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, i, u64p, vp]
-    L.spt_pack_pixels_async.argtypes = [vp, vp, i, i, i, i, vp]
+    if hasattr(L, "spt_pack_pixels_async"):   # (absent from older A/B builds under RT_HIP_LIB)
+        L.spt_pack_pixels_async.argtypes = [vp, vp, i, i, i, i, vp]
     L.spt_seed_fill.restype = None
     _lib = L
     return L
