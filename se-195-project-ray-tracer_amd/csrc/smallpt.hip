@@ -477,9 +477,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
 #endif
             }
             bool done = false, lights = false, a_R = false;
-            v3 normal, nd;                 // REFR: the hit's normal and reflected direction
-            float dp = 0.f, inv_sign = 1.f;
-            float4 oc = make_float4(0.f, 0.f, 0.f, 0.f);
+            float dp = 0.f, inv_sign = 1.f;  // REFR (pass A): vdot(normal, ray.d), -1 * sign(dp); and id
             if (shadow) {                                       // :154-161
                 SPT_PROF(PB_SHADOW);
                 cnt.isectp++;
@@ -498,11 +496,10 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     done = true;
                 } else {
                     SPT_PROF(PB_NEAREST);
-                    const float4 og = S.geo[id], oe = S.emi[id];
-                    oc = S.col[id];
+                    const float4 og = S.geo[id], oe = S.emi[id], oc = S.col[id];
                     hit = vsmul(t, ray.d);
                     hit = vadd(ray.o, hit);
-                    normal = vsub(hit, mk(og.x, og.y, og.z));
+                    v3 normal = vsub(hit, mk(og.x, og.y, og.z));
                     normal = vnorm(normal);
                     dp = vdot(normal, ray.d);
                     inv_sign = -1.f * (dp > 0 ? 1.f : -1.f);
@@ -522,19 +519,18 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                         lsum = mk(0.f, 0.f, 0.f);
                         li = 0;
                         lights = true;
-                    } else {
+                    } else if (refl == SPEC) {
+                        SPT_PROF(PB_SPEC);
                         specular = true;
-                        nd = vsmul(2.f * vdot(normal, ray.d), normal);
+                        v3 nd = vsmul(2.f * vdot(normal, ray.d), normal);
                         nd = vsub(ray.d, nd);
-                        if (refl == SPEC) {
-                            SPT_PROF(PB_SPEC);
-                            thr = vmul(thr, mk(oc.x, oc.y, oc.z));
-                            ray.o = hit;
-                            ray.d = nd;
-                        } else {
-                            SPT_PROF(PB_REFR);
-                            a_R = true;
-                        }
+                        thr = vmul(thr, mk(oc.x, oc.y, oc.z));
+                        ray.o = hit;
+                        ray.d = nd;
+                    } else {
+                        SPT_PROF(PB_REFR);
+                        specular = true;
+                        a_R = true;                             // ray, hit, nl, dp, inv_sign, id -> pass A
                     }
                     depth++;
                     done = done || (!lights && !a_R && depth > 6);   // :184 at the next bounce
@@ -551,15 +547,6 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             bool a_L = lights && li < S.nlights;
             bool lights_done = lights && !a_L;
             const bool was_R = a_R;
-            // nl = inv_sign * normal with inv_sign = +-1, so (rounding being
-            // sign-symmetric) vdot(normal, nl) = inv_sign * |n|^2 and
-            // vdot(ray.d, nl) = inv_sign * dp exactly: into is dp <= 0 (false
-            // for NaN, as the reference's NaN dot) and ddn is dp signed.
-            const bool into = dp <= 0.f;
-            const float nnt = into ? nc / nt : nt / nc;
-            const float ddn = inv_sign * dp;
-            const float cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
-            const bool tir = cos2t < 0.f;
             // One pass for every lane that needs A, then further light-only
             // passes while some lane skipped a light (scenes with several
             // lights).  The body is one lambda instantiated twice so the
@@ -573,6 +560,18 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                         lg = S.lrec[3 * li];                    // centre
                         lc = S.lrec[3 * li + 1];                // colour.xyz, rad
                     }
+                    // REFR terms (:281-296), rebuilt here from the few values
+                    // kept since the hit: normal = inv_sign * nl exactly
+                    // (inv_sign = +-1), and, rounding being sign-symmetric,
+                    // vdot(normal, nl) = inv_sign * |n|^2 and vdot(ray.d, nl) =
+                    // inv_sign * dp exactly: into is dp <= 0 (false for NaN, as
+                    // the reference's NaN dot) and ddn is dp signed.
+                    const v3 normal = vsmul(inv_sign, nl);
+                    const bool into = dp <= 0.f;
+                    const float nnt = into ? nc / nt : nt / nc;
+                    const float ddn = inv_sign * dp;
+                    const float cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
+                    const bool tir = cos2t < 0.f;
                     float x1 = 0.f, x2 = 0.f;
                     if (a_L || (with_r && !tir)) x1 = get_random(s0, s1);   // L: u2; R: the roulette draw
                     if (a_L) x2 = get_random(s0, s1);           // L: u1
@@ -629,6 +628,9 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                             lights_done = !a_L;
                         }
                     } else {
+                        const float4 oc = S.col[id];
+                        v3 nd = vsmul(2.f * dp, normal);         // vdot(normal, ray.d) = dp
+                        nd = vsub(ray.d, nd);
                         ray.o = hit;
                         if (tir) {
                             thr = vmul(thr, mk(oc.x, oc.y, oc.z));
