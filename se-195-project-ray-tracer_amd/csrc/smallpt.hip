@@ -325,6 +325,9 @@ __device__ __forceinline__ int to_int(float x)
 #ifndef RT_SPT_QUNROLL
 #define RT_SPT_QUNROLL 3
 #endif
+#ifndef RT_SPT_PRIO
+#define RT_SPT_PRIO 1       // progress-levelled s_setprio (A/B: 0 = off)
+#endif
 #ifndef RT_SPT_MINWAVES
 #define RT_SPT_MINWAVES 1   // __launch_bounds__ min waves per SIMD (occupancy A/B builds)
 #endif
@@ -415,6 +418,10 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         int k = 0;
         bool need_cam = nsamples > 0, need_bounce = false;
         constexpr float nc = 1.f, nt = 1.5f;
+#if RT_SPT_PRIO
+        int prio_level = 0, prio_next = nsamples / 4;
+        __builtin_amdgcn_s_setprio(3);
+#endif
         while (true) {
             // ---- pass B: DIFF bounce (geomfunc.h:229-269) or camera ray
             // (smallptCPU.cpp:89-105).  Both draw two randoms and normalise
@@ -458,6 +465,22 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 need_bounce = need_cam = false;
             }
             if (k >= nsamples) break;
+#if RT_SPT_PRIO
+            // Progress-levelled issue priority.  The SIMD arbitrates VALU issue
+            // by priority, then age, so waves that start together finish one
+            // after another and the last one runs alone at a fraction of the
+            // SIMD's rate.  A wave whose every lane has passed another quarter
+            // of its samples drops one priority level, letting the waves
+            // behind it catch up: co-resident waves stay level and finish
+            // together.  (s_setprio only reorders issue; results unchanged.)
+            if (!wave_any(k < prio_next)) {
+                prio_level++;
+                prio_next = (prio_level + 1) * nsamples / 4;
+                if (prio_level == 1) __builtin_amdgcn_s_setprio(2);
+                else if (prio_level == 2) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+#endif
 
             SPT_PROF(PB_ITER);
 #ifdef RT_SPT_TRACE
