@@ -40,13 +40,21 @@ constexpr int DIFF = 0, SPEC = 1;   // REFR = 2 is the remaining case
 
 struct SphereGeo { float4 g; };          // centre.xyz, rad*rad (same float product as :42)
 
-__device__ __forceinline__ float get_random(uint32_t &s0, uint32_t &s1)   // simplernd.h:34-48
+// GetRandom, simplernd.h:34-48, returning f = the float in [2, 4) that the
+// reference maps to (f - 2) / 2.  Callers finish with fma(f, .5, c): for
+// c = -1 that is (f - 2) / 2 and for c = -1.5 it is (f - 2) / 2 - .5f, exact
+// (f / 2 - 1 and f / 2 - 1.5 are representable, as are the reference's two
+// steps each), in one op instead of two or three.
+__device__ __forceinline__ float get_random_f(uint32_t &s0, uint32_t &s1)
 {
     s0 = 36969u * (s0 & 65535u) + (s0 >> 16);
     s1 = 18000u * (s1 & 65535u) + (s1 >> 16);
     const uint32_t ires = (s0 << 16) + s1;
-    const float f = __uint_as_float((ires & 0x007fffffu) | 0x40000000u);
-    return (f - 2.f) / 2.f;
+    return __uint_as_float((ires & 0x007fffffu) | 0x40000000u);
+}
+__device__ __forceinline__ float get_random(uint32_t &s0, uint32_t &s1)
+{
+    return __builtin_fmaf(get_random_f(s0, s1), .5f, -1.f);
 }
 
 __device__ __forceinline__ float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
@@ -428,15 +436,15 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             // one vector.
             if (need_bounce || need_cam) {
                 SPT_PROF(PB_BOUNCE);
-                const float x1 = get_random(s0, s1);
-                const float x2 = get_random(s0, s1);
+                const float f1 = get_random_f(s0, s1), f2 = get_random_f(s0, s1);
+                const float x1 = __builtin_fmaf(f1, .5f, -1.f), x2 = __builtin_fmaf(f2, .5f, -1.f);
                 // bounce: r1 = 2 PI x1, r2 = x2, u = norm(a x w)
                 const v3 wv = nl;
                 const v3 a = (fabsf(wv.x) > .1f) ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
                 const v3 cu = vxcross(a, wv);
                 // camera: r1 = x1 - .5, r2 = x2 - .5
-                const float kcx = (x + (x1 - .5f)) * invW - .5f;
-                const float kcy = (y + (x2 - .5f)) * invH - .5f;
+                const float kcx = (x + __builtin_fmaf(f1, .5f, -1.5f)) * invW - .5f;   // r1 = GetRandom() - .5f
+                const float kcy = (y + __builtin_fmaf(f2, .5f, -1.5f)) * invH - .5f;
                 const v3 rdir = mk(cam.x.x * kcx + cam.y.x * kcy + cam.dir.x,
                                    cam.x.y * kcx + cam.y.y * kcy + cam.dir.y,
                                    cam.x.z * kcx + cam.y.z * kcy + cam.dir.z);
