@@ -11,7 +11,10 @@ assembles the HDR accumulator and the RGBA8 frame on every rank.
 Rows are sharded over ranks in equal contiguous bands (strong scaling: the
 frame is fixed, each of N GPUs renders 1/N of it); for N > 1 one in-place
 RCCL all-gather of the HDR accumulator per frame, then every rank repacks the
-RGBA8 frame from it (spt_pack_pixels_async).  Rays = Intersect +
+RGBA8 frame from it (spt_pack_pixels_async).  Frames are pipelined: frame
+i+1 renders while frame i is gathered (double-buffered frame, second stream).
+After the timed steps, rank 0's assembled frame is checked bit for bit
+against one GPU rendering the whole frame ("frame_check").  Rays = Intersect +
 IntersectP calls, counted by the kernel itself.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-whitted]
@@ -221,33 +224,58 @@ def main():
 
     spheres, ns = rtamd.scenes.cornell()
     cam = rtamd.scenes.cornell_camera(W, H)
-    scene = rtamd.SmallptScene(spheres, ns)       # uploaded once, SGPR geometry packed
+    scene = rtamd.SmallptScene(spheres, ns)       # uploaded once
     seeds0 = torch.from_numpy(rtamd.scenes.seeds(W, H).view(np.int32)).to(dev)  # pristine
     seeds = torch.empty_like(seeds0)
-    colors = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
-    pixels = torch.zeros(W * H, dtype=torch.int32, device=dev)
     cnt = torch.zeros(4, dtype=torch.int64, device=dev)
     r0, r1 = rdist.row_band(rank, world, H)
     B = r1 - r0
     s = torch.cuda.current_stream(dev)
-    def pack():                  # RGBA8 frame from the gathered HDR accumulator (toInt, bit-exact)
-        rtamd.check(L.spt_pack_pixels_async(colors.data_ptr(), pixels.data_ptr(), W, H, 0, H, s.cuda_stream))
+    # N > 1 over RCCL: frames are pipelined -- frame i+1 renders (stream s)
+    # while frame i's HDR all-gather and RGBA8 repack run on a second stream,
+    # with the frame buffers double-buffered (a buffer is rendered into again
+    # only after its previous gather finished).  Each rank's progressive state
+    # is its own band, so frame i+1 never needs frame i's gathered frame.
+    pipelined = distributed and (backend == "nccl" or os.environ.get("RT_BENCH_PIPELINE") == "1") and \
+        not os.environ.get("RT_BENCH_NO_PIPELINE")
+    nbuf = 2 if pipelined else 1
+    colors = [torch.zeros(3 * W * H, dtype=torch.float32, device=dev) for _ in range(nbuf)]
+    pixels = [torch.zeros(W * H, dtype=torch.int32, device=dev) for _ in range(nbuf)]
+    gs = torch.cuda.Stream(dev) if pipelined else s
 
-    gather = rdist.FrameGather(colors, pixels, rank, world, W, H, pack=pack)
+    def packer(b):               # RGBA8 frame from the gathered HDR accumulator (toInt, bit-exact)
+        def pack():
+            rtamd.check(L.spt_pack_pixels_async(colors[b].data_ptr(), pixels[b].data_ptr(), W, H, 0, H,
+                                                torch.cuda.current_stream(dev).cuda_stream))
+        return pack
+
+    gathers = [rdist.FrameGather(colors[b], pixels[b], rank, world, W, H, pack=packer(b)) for b in range(nbuf)]
+    freed = [None] * nbuf        # event: buffer b's last gather finished
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
+    nframe = [0]
 
     def step(i=None, counters=None):
+        b = nframe[0] % nbuf
+        nframe[0] += 1
+        if freed[b] is not None:
+            s.wait_event(freed[b])
         if i is not None:
             ev[i][0].record(s)
-        rtamd.check(L.spt_scene_render_async(scene.handle, C.byref(cam), colors.data_ptr(),
-                                       seeds0.data_ptr(), seeds.data_ptr(), pixels.data_ptr(), W, H, r0, r1,
-                                       0, SPP, rtamd.SPT_PATH_TRACING,
-                                       counters.data_ptr() if counters is not None else None,
-                                       s.cuda_stream))
+        rtamd.check(L.spt_scene_render_async(scene.handle, C.byref(cam), colors[b].data_ptr(),
+                                             seeds0.data_ptr(), seeds.data_ptr(), pixels[b].data_ptr(), W, H,
+                                             r0, r1, 0, SPP, rtamd.SPT_PATH_TRACING,
+                                             counters.data_ptr() if counters is not None else None,
+                                             s.cuda_stream))
         if i is not None:
             ev[i][1].record(s)
-        gather.gather()          # RCCL all-gather of the HDR bands + RGBA8 repack (no-op at N=1)
+        if world > 1:            # RCCL all-gather of the HDR bands + RGBA8 repack
+            gs.wait_stream(s)
+            with torch.cuda.stream(gs):
+                gathers[b].gather()
+            if pipelined:
+                freed[b] = torch.cuda.Event()
+                freed[b].record(gs)
 
     for _ in range(args.warmup):
         step()
@@ -300,7 +328,8 @@ def main():
         "data": "synthetic: reference Cornell scene (scene.h:29-40), glibc rand() seeds, random-free camera",
         "config": {"workload": "smallpt Cornell 1920x1080 64spp RadiancePathTracing, one frame per step",
                    "frame": [W, H], "spp": SPP, "spheres": ns, "rows_per_gpu": B,
-                   "parallelism": "row bands x%d + RCCL HDR all-gather" % world if world > 1 else "single GPU"},
+                   "parallelism": ("row bands x%d + RCCL HDR all-gather%s" % (world, " (pipelined)" if pipelined else ""))
+                   if world > 1 else "single GPU"},
         "frames_per_s": round(1e3 / ms_per_step, 3),
         "Msamples_per_s": round(W * H * SPP / (ms_per_step * 1e-3) / 1e6, 2),
         "rays_per_frame": rays_per_frame,
@@ -321,6 +350,21 @@ def main():
                  "issue_basis": "SQ_INSTS_VALU x 2 cycles (wave64 on SIMD32) / (1024 SIMDs x 2.4 GHz x "
                                 "kernel time), from the PMC digest"},
     }
+    if distributed:
+        # Self-check of the sharded path (outside the timed region): the last
+        # assembled frame must equal one GPU rendering the whole frame.
+        last = (nframe[0] - 1) % nbuf
+        ref_c = torch.zeros_like(colors[0])
+        ref_p = torch.zeros_like(pixels[0])
+        ref_s = torch.empty_like(seeds0)
+        rtamd.check(L.spt_scene_render_async(scene.handle, C.byref(cam), ref_c.data_ptr(), seeds0.data_ptr(),
+                                             ref_s.data_ptr(), ref_p.data_ptr(), W, H, 0, H, 0, SPP,
+                                             rtamd.SPT_PATH_TRACING, None, s.cuda_stream))
+        torch.cuda.synchronize(dev)
+        ok = torch.tensor([int(torch.equal(ref_c.view(torch.int32), colors[last].view(torch.int32))
+                               and torch.equal(ref_p, pixels[last]))], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        out["frame_check"] = "assembled frame == single-GPU frame (bit-exact)" if ok.item() else "MISMATCH"
     if rank == 0 and world == 1:
         if not args.no_whitted:
             out["whitted"] = whitted_line(args, dev)
