@@ -182,10 +182,14 @@ __device__ __forceinline__ int query_bf(const G &geo, const ray3 &r, float &t, i
 //   * a direction with |d|^2 = 1 + e puts the formula's roots on a sphere of
 //     radius sqrt(r^2 + e t*^2), i.e. sqrt(e) * t* further out.
 // With |op| <= |o - C| + R, r <= R and t* <= |o - C| + 2R this is below
-// alpha * |o - C| + BVH_ALPHA_R * R + BETA for alpha = 1/128 when e < 2^-20
-// (rays here are normalised or built from unit vectors: e ~ 1e-7), alpha =
-// 1/16 when e < 2^-9, and no culling at all beyond; each is more than three
-// times the bound.  So a node whose box, grown by m on every side, is not
+// (1.04e-3 + sqrt(e)) |o - C| + (1.04e-3 + 2 sqrt(e)) R.  The margin is
+// alpha * |o - C| + BVH_ALPHA_R * R + BETA with a per-ray alpha = 2 x
+// (1.04e-3 + sqrt(e' + 2^-22)) (e' the float-computed e, whose rounding the
+// 2^-22 covers): twice the bound's first coefficient; BVH_ALPHA_R = 1/64 is
+// 1.7 .. 7x the second for e < 2^-16, and beyond that nothing is culled
+// (rays here are normalised or built from unit vectors: e ~ 1e-7, alpha ~
+// 1/270).  tests/test_bvh_margin.py measures the float roots of grazing rays
+// at ~0.57 of the bound.  So a node whose box, grown by m on every side, is not
 // crossed by the ray between 0 and lim (the current nearest distance, or
 // maxt) holds no sphere that could be taken; its spheres are skipped.  BETA
 // and the same slack absorb the slab test's own rounding (approximate
@@ -201,6 +205,13 @@ struct BvhView {
     int nalways, nnodes;
 };
 constexpr float BVH_ALPHA_R = 1.f / 64.f;   // per node, with BETA, in the node record
+#ifndef RT_BVH_K
+#define RT_BVH_K 2.f
+#endif
+#ifndef RT_BVH_BATCH
+#define RT_BVH_BATCH 32     // leaf postponement: test pending leaves once >= BATCH/64 of the walking lanes hold one
+#endif
+constexpr float BVH_K = RT_BVH_K;           // per-ray alpha: K x the bound's |o - C| coefficient
 constexpr int BVH_LEAF_MAX = 4;             // spheres per leaf (host build: BVH_LEAF)
 
 // One ray query through the hierarchy.  Nearest hit (shadow = false): t in
@@ -216,9 +227,27 @@ constexpr int BVH_LEAF_MAX = 4;             // spheres per leaf (host build: BVH
 // indices before the first test, so a step costs one memory latency (a first
 // form that branched on the link word first and loaded per sphere paid two
 // to five: configs[4] 11.1 -> 8.5 ms per 4 spp).
+// Tools-only traversal statistics (build with -DRT_BVH_STATS; read by
+// spt_bvh_stats_read): lane node visits, lane crossed leaves, lane sphere
+// tests, wave loop trips, wave leaf-block executions, lane queries, wave
+// queries.  Never in the product build.
+#ifdef RT_BVH_STATS
+__device__ unsigned long long g_bvh_stats[24];
+#define BVH_ST(k, v) st[k] += (v)
+#define BVH_ST_WAVE(k) do { if ((int)(threadIdx.x & 63) == __builtin_ctzll(__builtin_amdgcn_read_exec())) st[k]++; } while (0)
+#else
+#define BVH_ST(k, v) do {} while (0)
+#define BVH_ST_WAVE(k) do {} while (0)
+#endif
+
 template <bool COUNT>
 __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
 {
+#ifdef RT_BVH_STATS
+    unsigned st[24] = {};
+    BVH_ST(5, 1);
+    BVH_ST_WAVE(6);
+#endif
     const float maxt = t;
     int id = -1;
     bool stop = false;
@@ -242,55 +271,94 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
     const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
     const float ax = fabsf(ix), ay = fabsf(iy), az = fabsf(iz);
     const float e = fabsf(r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z - 1.f);
-    const float alpha = e < 0x1p-20f ? 1.f / 128.f : (e < 0x1p-9f ? 1.f / 16.f : 1e30f);
+    const float alpha = e < 0x1p-16f ? BVH_K * (1.04e-3f + __builtin_amdgcn_sqrtf(e + 0x1p-22f)) : 1e30f;
     // Layout of this ray's direction octant: near children first.
     const float4 *nodes = B.node + 2 * (size_t)B.nnodes *
                                        ((dx < 0.f ? 1 : 0) | (dy < 0.f ? 2 : 0) | (dz < 0.f ? 4 : 0));
+    // Crossed leaves are postponed: a lane that reaches one stops stepping
+    // and keeps it pending; the wave tests the pending leaves' spheres
+    // together once at least RT_BVH_BATCH/64 of its lanes still in the walk
+    // hold one (or none can step), instead of running the leaf block for the
+    // one or two lanes that reach a leaf in a given step.  Spheres are tested
+    // in the same per-lane order, so results are unchanged.
     int node = stop ? B.nnodes : 0;
-    while (node < B.nnodes) {
-        const float4 a = nodes[2 * node], b = nodes[2 * node + 1];
-        const int link = __float_as_int(a.w);
-        const float lim = shadow ? maxt : t;
-        const float cx = a.x - r.o.x, cy = a.y - r.o.y, cz = a.z - r.o.z;
-        const float dist = __builtin_amdgcn_sqrtf(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, cz * cz)));
-        const float m = __builtin_fmaf(alpha, dist, b.w);
-        const float tcx = cx * ix, tcy = cy * iy, tcz = cz * iz;                // slab centres
-        const float hx = (b.x + m) * ax, hy = (b.y + m) * ay, hz = (b.z + m) * az;  // slab half-widths
-        const float tn = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
-        const float tf = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
-        const bool cross = tn <= tf && tf >= 0.f && tn <= lim;
-        int next = cross ? node + 1 : link;
-        if (link < 0) {                                  // leaf ~(first | count << 24); escape = next node
-            next = node + 1;
-            if (cross) {
-                const int info = ~link;
-                const int f = info & 0xffffff, c = info >> 24;
-                float4 g[BVH_LEAF_MAX];
-                int gi[BVH_LEAF_MAX];
+    int pend = 0;                                         // pending leaf info (first | count << 24), 0 = none
+    while (true) {
+        if (node < B.nnodes && pend == 0) {
+            BVH_ST(0, 1);
+            BVH_ST_WAVE(3);
+            const float4 a = nodes[2 * node], b = nodes[2 * node + 1];
+            const int link = __float_as_int(a.w);
+            const float lim = shadow ? maxt : t;
+            const float cx = a.x - r.o.x, cy = a.y - r.o.y, cz = a.z - r.o.z;
+            const float dist = __builtin_amdgcn_sqrtf(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, cz * cz)));
+            const float m = __builtin_fmaf(alpha, dist, b.w);
+            const float tcx = cx * ix, tcy = cy * iy, tcz = cz * iz;                // slab centres
+            const float hx = (b.x + m) * ax, hy = (b.y + m) * ay, hz = (b.z + m) * az;  // slab half-widths
+            const float tn = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
+            const float tf = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
+            const bool cross = tn <= tf && tf >= 0.f && tn <= lim;
+            int next = cross ? node + 1 : link;
+            if (link < 0) {                              // leaf ~(first | count << 24); escape = next node
+                next = node + 1;
+                if (cross) pend = ~link;
+            }
+            node = next;
+        }
+        const unsigned long long pm = __builtin_amdgcn_ballot_w64(pend != 0);
+        const unsigned long long sm = __builtin_amdgcn_ballot_w64(node < B.nnodes && pend == 0);
+        if (pm == 0) {
+            if (sm == 0) break;
+            continue;
+        }
+        if (sm != 0 && 64 * __builtin_popcountll(pm) < RT_BVH_BATCH * __builtin_popcountll(pm | sm)) continue;
+        if (pend != 0) {
+            const int f = pend & 0xffffff, c = pend >> 24;
+            BVH_ST(1, 1);
+            BVH_ST(2, c);
+            BVH_ST_WAVE(4);
+            float4 g[BVH_LEAF_MAX];
+            int gi[BVH_LEAF_MAX];
 #pragma unroll
-                for (int q = 0; q < BVH_LEAF_MAX; q++) {  // all loads first: one latency per leaf
-                    const int j = f + (q < c ? q : 0);
-                    g[q] = B.geo[j];
-                    gi[q] = B.id[j];
-                }
+            for (int q = 0; q < BVH_LEAF_MAX; q++) {      // all loads first: one latency per leaf
+                const int j = f + (q < c ? q : 0);
+                g[q] = B.geo[j];
+                gi[q] = B.id[j];
+            }
 #pragma unroll
-                for (int q = 0; q < BVH_LEAF_MAX; q++) {
-                    if (q < c) {
-                        const float d = sphere_hit(g[q], r);
-                        const int i = gi[q];
-                        if (shadow) {
-                            if (d < maxt && i > id) id = i;
-                        } else if (d < t || (d == t && i > id)) {
-                            t = d;
-                            id = i;
-                        }
+            for (int q = 0; q < BVH_LEAF_MAX; q++) {
+                if (q < c) {
+                    const float d = sphere_hit(g[q], r);
+                    const int i = gi[q];
+                    if (shadow) {
+                        if (d < maxt && i > id) id = i;
+                    } else if (d < t || (d == t && i > id)) {
+                        t = d;
+                        id = i;
                     }
                 }
-                if (!COUNT && shadow && id >= 0) next = B.nnodes;
             }
+            if (!COUNT && shadow && id >= 0) node = B.nnodes;
+            pend = 0;
         }
-        node = next;
     }
+#ifdef RT_BVH_STATS
+    {
+        const float4 a0 = nodes[0], b0 = nodes[1];
+        const bool far = fabsf(r.o.x - a0.x) > b0.x || fabsf(r.o.y - a0.y) > b0.y || fabsf(r.o.z - a0.z) > b0.z;
+        st[7] = st[0] >= 128; st[8] = st[0] >= 512; st[9] = st[0] >= 2048;
+        st[10] = far ? st[0] : 0; st[11] = far; st[12] = shadow; st[13] = shadow ? st[0] : 0;
+        st[14] = far && st[0] >= 512;
+        st[15] = alpha > 1.f / 128.f; st[16] = st[15] ? st[0] : 0;
+        const float ox = r.o.x - a0.x, oy = r.o.y - a0.y, oz = r.o.z - a0.z;
+        const float R0 = sqrtf(b0.x * b0.x + b0.y * b0.y + b0.z * b0.z);
+        const bool vfar = ox * ox + oy * oy + oz * oz > 64.f * R0 * R0;
+        st[17] = vfar; st[18] = vfar ? st[0] : 0; st[19] = vfar && st[0] >= 512; st[20] = st[15] && st[0] >= 512;
+    }
+#pragma unroll
+    for (int k = 0; k < 21; k++)
+        if (st[k]) atomicAdd(&g_bvh_stats[k], (unsigned long long)st[k]);   // divergent: per-lane atomics
+#endif
     return id;
 }
 
@@ -1202,6 +1270,17 @@ extern "C" int spt_prof_read(unsigned long long *out)
     static const unsigned long long zero[2 * rt::smallpt::PB_N] = {};
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(rt::smallpt::g_spt_prof), zero, sizeof(zero));
     return e == hipSuccess ? RT_OK : rtrt::fail_hip(e, "spt_prof_read");
+}
+#endif
+
+#ifdef RT_BVH_STATS
+// Tools-only: reads and clears the traversal statistics (16 counters).
+extern "C" int spt_bvh_stats_read(unsigned long long *out)
+{
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(rt::smallpt::g_bvh_stats), sizeof(rt::smallpt::g_bvh_stats));
+    static const unsigned long long zero[24] = {};
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(rt::smallpt::g_bvh_stats), zero, sizeof(zero));
+    return e == hipSuccess ? RT_OK : rtrt::fail_hip(e, "spt_bvh_stats_read");
 }
 #endif
 

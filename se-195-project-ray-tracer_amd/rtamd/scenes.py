@@ -116,11 +116,12 @@ def _cross(a, b):
                      f32(a[0] * b[1]) - f32(a[1] * b[0])], dtype=f32)
 
 
-def update_camera(cam, width, height):
+def update_camera(cam, width, height, fov_deg=45.0):
     """UpdateCamera (displayfunc.cpp:182-195): fov = (M_PI/180.f)*45.f in
-    double, narrowed; x scaled by width*fov/height (float)."""
+    double, narrowed; x scaled by width*fov/height (float).  fov_deg other
+    than the reference's 45 is for tests (narrow views of far scenes)."""
     d = _norm(_v(cam.target) - _v(cam.orig))
-    fov = f32((math.pi / float(f32(180.0))) * 45.0)
+    fov = f32((math.pi / float(f32(180.0))) * fov_deg)
     x = _norm(_cross(d, np.array([0, 1, 0], dtype=f32)))
     k = f32(f32(f32(width) * fov) / f32(height))
     x = np.array([k * x[0], k * x[1], k * x[2]], dtype=f32)

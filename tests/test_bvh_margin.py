@@ -1,33 +1,46 @@
 """Empirical check of the error bound behind the sphere hierarchy's culling
-margin (smallpt.hip, BvhView comment): for grazing rays the point at the
-float32 SphereIntersect distance (geomfunc.h:32-59 arithmetic, no FMA) lies
-within 1.04e-3 * max(|op|, r) of the sphere (the analytical bound), far below
-the 1/128 the traversal uses."""
+margin (smallpt.hip, BvhView comment): the point at the float32
+SphereIntersect distance t (geomfunc.h:32-59 arithmetic, no FMA) of a
+vnorm-normalised direction d, |d|^2 = 1 + e, lies within
+1.04e-3 * max(|op|, r) + sqrt(e) * t of the sphere -- the analytical bound,
+which the traversal's per-ray margin coefficient 2 * (1.04e-3 + sqrt(e +
+2^-22)) doubles.  Rays are aimed at grazing incidence (the worst case) from
+near and far origins."""
 import numpy as np
 
 
 def test_float_root_within_margin_bound():
-    rng = np.random.default_rng(7)
-    n = 400_000
     f = np.float32
-    c = rng.uniform(-300, 300, (n, 3)).astype(f)
-    r = (10 ** rng.uniform(-2, 3, n)).astype(f)
-    o = rng.uniform(-300, 300, (n, 3)).astype(f)
-    u = rng.standard_normal((n, 3))
-    u /= np.linalg.norm(u, axis=1, keepdims=True)
-    tgt = c.astype(np.float64) + r[:, None] * (1 + rng.uniform(-1e-3, 1e-3, n))[:, None] * u
-    d = tgt - o.astype(np.float64)
-    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(f)
-    op = (c - o).astype(f)
-    b = ((op[:, 0] * d[:, 0] + op[:, 1] * d[:, 1]).astype(f) + op[:, 2] * d[:, 2]).astype(f)
-    oo = ((op[:, 0] * op[:, 0] + op[:, 1] * op[:, 1]).astype(f) + op[:, 2] * op[:, 2]).astype(f)
-    det = (((b * b).astype(f) - oo).astype(f) + (r * r).astype(f)).astype(f)
-    ok = det >= 0
-    t1 = (b[ok] - np.sqrt(det[ok]).astype(f)).astype(f)
-    P = o[ok].astype(np.float64) + t1[:, None].astype(np.float64) * d[ok].astype(np.float64)
-    C = c[ok].astype(np.float64)
-    R = r[ok].astype(np.float64)
-    off = np.abs(np.linalg.norm(P - C, axis=1) - R)
-    scale = np.maximum(np.linalg.norm(C - o[ok].astype(np.float64), axis=1), R)
-    assert ok.sum() > n // 4
-    assert (off / scale).max() < 1.04e-3 < (1 / 128) / 3
+    worst = 0.0
+    for seed, span in ((7, 300.0), (8, 3000.0), (9, 30000.0)):
+        rng = np.random.default_rng(seed)
+        n = 300_000
+        c = rng.uniform(-span, span, (n, 3)).astype(f)
+        r = (10 ** rng.uniform(-2, 3, n)).astype(f)
+        o = rng.uniform(-span, span, (n, 3)).astype(f)
+        u = rng.standard_normal((n, 3))
+        u /= np.linalg.norm(u, axis=1, keepdims=True)
+        graze = 1 + rng.uniform(-1e-2, 1e-2, n) * 10 ** rng.uniform(-6, 0, n)
+        tgt = c.astype(np.float64) + (r * graze)[:, None] * u
+        d32 = (tgt - o.astype(np.float64)).astype(f)
+        dd = ((d32[:, 0] * d32[:, 0] + d32[:, 1] * d32[:, 1]).astype(f) + d32[:, 2] * d32[:, 2]).astype(f)
+        d = (d32 * (f(1) / np.sqrt(dd).astype(f)).astype(f)[:, None]).astype(f)      # vnorm
+        op = (c - o).astype(f)
+        b = ((op[:, 0] * d[:, 0] + op[:, 1] * d[:, 1]).astype(f) + op[:, 2] * d[:, 2]).astype(f)
+        oo = ((op[:, 0] * op[:, 0] + op[:, 1] * op[:, 1]).astype(f) + op[:, 2] * op[:, 2]).astype(f)
+        det = (((b * b).astype(f) - oo).astype(f) + (r * r).astype(f)).astype(f)
+        ok = det >= 0
+        assert ok.sum() > n // 4
+        sd = np.sqrt(det[ok]).astype(f)
+        for t in ((b[ok] - sd).astype(f), (b[ok] + sd).astype(f)):
+            g = t > 0.01
+            dg = d[ok][g].astype(np.float64)
+            og = o[ok][g].astype(np.float64)
+            C = c[ok][g].astype(np.float64)
+            R = r[ok][g].astype(np.float64)
+            P = og + t[g, None].astype(np.float64) * dg
+            off = np.abs(np.linalg.norm(P - C, axis=1) - R)
+            e = np.abs((dg * dg).sum(1) - 1)
+            bound = 1.04e-3 * np.maximum(np.linalg.norm(C - og, axis=1), R) + np.sqrt(e) * t[g]
+            worst = max(worst, float((off / bound).max()))
+    assert worst < 0.75      # measured ~0.57: the bound holds with room; the margin doubles it

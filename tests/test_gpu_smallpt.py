@@ -174,11 +174,14 @@ def test_bvh_equals_full_scan_configs4(rt, monkeypatch):
     _bvh_vs_scan(rt, monkeypatch, spheres, n, cam, 1920, 1080, 2)
 
 
-@pytest.mark.parametrize("seed,mode", [(1, 0), (2, 0), (3, 1), (4, 0)])
-def test_bvh_equals_full_scan_random_scenes(rt, monkeypatch, seed, mode):
+@pytest.mark.parametrize("seed,mode,far", [(1, 0, 0), (2, 0, 0), (3, 1, 0), (4, 0, 0),
+                                           (5, 0, 3000), (6, 1, 20000)])
+def test_bvh_equals_full_scan_random_scenes(rt, monkeypatch, seed, mode, far):
     """Random clouds of small spheres (some overlapping, some tiny, some far),
     a huge ground sphere and lights, camera inside the cloud: grazing and
-    inside-sphere rays included."""
+    inside-sphere rays included.  far > 0: camera that far away with a
+    narrow view of the cloud, where the culling margin (proportional to the
+    origin's distance) is widest in absolute terms."""
     rng = np.random.default_rng(seed)
     n = 3000
     S = (rt.Sphere * n)()
@@ -192,9 +195,9 @@ def test_bvh_equals_full_scan_random_scenes(rt, monkeypatch, seed, mode):
         refl = int(rng.choice([DIFF, DIFF, DIFF, SPEC, REFR]))
         rt.scenes._sphere(S[i], scale, tuple(c), (0, 0, 0), tuple(rng.uniform(0.2, 0.9, 3)), refl)
     cam = rt.Camera()
-    cam.orig = rt.Vec3(1.0, 2.0, 25.0)
+    cam.orig = rt.Vec3(1.0, 2.0, 25.0) if not far else rt.Vec3(0.3 * far, 0.2 * far, far)
     cam.target = rt.Vec3(0.0, 0.0, 0.0)
-    rt.scenes.update_camera(cam, 160, 120)
+    rt.scenes.update_camera(cam, 160, 120, fov_deg=45.0 if not far else 45.0 * 60.0 / far)
     _bvh_vs_scan(rt, monkeypatch, S, n, cam, 160, 120, 4, mode)
 
 

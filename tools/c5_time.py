@@ -31,9 +31,25 @@ def run(c=None):
                                          c.data_ptr() if c is not None else None, st.cuda_stream))
 
 
+stats = getattr(L, "spt_bvh_stats_read", None)   # RT_BVH_STATS builds only
+bs = (C.c_ulonglong * 24)()
+if stats:
+    stats(bs)
 run(cnt)
 torch.cuda.synchronize()
 rays = int(cnt[0] + cnt[1])
+if stats:
+    stats(bs)
+    q, wq = max(bs[5], 1), max(bs[6], 1)
+    print("  bvh: per query %.2f nodes, %.2f crossed leaves, %.2f sphere tests; per wave-query %.2f loop trips, "
+          "%.2f leaf-block runs, %.1f lanes; node-step lane util %.3f, leaf-block lane util %.3f" % (
+              bs[0] / q, bs[1] / q, bs[2] / q, bs[3] / wq, bs[4] / wq, q / wq,
+              bs[0] / (64.0 * max(bs[3], 1)), bs[1] / (64.0 * max(bs[4], 1))))
+    print("  queries >= 128/512/2048 nodes: %d %d %d of %d; origin outside root box: %d queries, %.1f nodes each, "
+          "%d of them >= 512; shadow: %d queries, %.1f nodes each" % (
+              bs[7], bs[8], bs[9], bs[5], bs[11], bs[10] / max(bs[11], 1), bs[14], bs[12], bs[13] / max(bs[12], 1)))
+    print("  alpha != 1/128: %d queries, %.1f nodes each, %d >= 512; origin > 8 root radii away: %d queries, "
+          "%.1f nodes each, %d >= 512" % (bs[15], bs[16] / max(bs[15], 1), bs[20], bs[17], bs[18] / max(bs[17], 1), bs[19]))
 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 a.record(st)
 run()
