@@ -211,6 +211,9 @@ constexpr float BVH_ALPHA_R = 1.f / 64.f;   // per node, with BETA, in the node 
 #ifndef RT_BVH_BATCH
 #define RT_BVH_BATCH 32     // leaf postponement: test pending leaves once >= BATCH/64 of the walking lanes hold one
 #endif
+#ifndef RT_BVH_BUDGET
+#define RT_BVH_BUDGET 32    // walk steps per render-loop iteration before a lane's query is suspended
+#endif
 constexpr float BVH_K = RT_BVH_K;           // per-ray alpha: K x the bound's |o - C| coefficient
 constexpr int BVH_LEAF_MAX = 4;             // spheres per leaf (host build: BVH_LEAF)
 
@@ -240,17 +243,21 @@ __device__ unsigned long long g_bvh_stats[24];
 #define BVH_ST_WAVE(k) do {} while (0)
 #endif
 
+// A query's walk state, kept across loop iterations of render_kernel: the
+// walk is resumable, so a lane whose walk is long does not hold up the
+// other lanes of its wave (they shade and start their next queries while it
+// continues).  t = nearest distance so far (any hit: maxt, unchanged), id =
+// the result so far, node = next node in the ray's octant layout (nnodes:
+// finished), pend = a crossed leaf not yet tested (first | count << 24).
+struct BvhWalk { float t; int id, node, pend; };
+
+// Starts a query: the "always" spheres, then the walk from the root.
+// Nearest hit (shadow = false): t = 1e20f on entry; any hit: t = maxt.
 template <bool COUNT>
-__device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
+__device__ __forceinline__ void bvh_begin(const BvhView &B, const ray3 &r, bool shadow, float t, BvhWalk &W)
 {
-#ifdef RT_BVH_STATS
-    unsigned st[24] = {};
-    BVH_ST(5, 1);
-    BVH_ST_WAVE(6);
-#endif
     const float maxt = t;
     int id = -1;
-    bool stop = false;
     for (int k = 0; k < B.nalways; k++) {
         const float d = sphere_hit(B.ageo[k], r);
         const int i = B.aid[k];
@@ -261,7 +268,29 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
             id = i;
         }
     }
-    if (!COUNT && shadow && id >= 0) stop = true;
+    W.t = t;
+    W.id = id;
+    W.node = (!COUNT && shadow && id >= 0) ? B.nnodes : 0;
+    W.pend = 0;
+}
+
+// Advances the walks of the wave's lanes by up to RT_BVH_BUDGET steps
+// (node visits); returns true for a lane whose query is complete: W.id is
+// then the nearest sphere (highest index on ties) with W.t its distance, or
+// for any hit an occluder index (COUNT: the highest one, IntersectP's
+// early-exit position, for the test counter; without COUNT the walk stops
+// at the first) or -1.
+template <bool COUNT>
+__device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &W)
+{
+#ifdef RT_BVH_STATS
+    unsigned st[24] = {};
+    BVH_ST(5, W.node == 0 && W.pend == 0);
+    BVH_ST_WAVE(6);
+#endif
+    const float maxt = W.t;
+    float t = W.t;
+    int id = W.id, node = W.node, pend = W.pend;
     // Slab test (culling only: its rounding is inside the margin; fused ops
     // are fine here and nowhere else).  Zero direction components become
     // +-1e-30 so no 0 * inf appears.
@@ -279,10 +308,10 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
     // and keeps it pending; the wave tests the pending leaves' spheres
     // together once at least RT_BVH_BATCH/64 of its lanes still in the walk
     // hold one (or none can step), instead of running the leaf block for the
-    // one or two lanes that reach a leaf in a given step.  Spheres are tested
-    // in the same per-lane order, so results are unchanged.
-    int node = stop ? B.nnodes : 0;
-    int pend = 0;                                         // pending leaf info (first | count << 24), 0 = none
+    // one or two lanes that reach a leaf in a given step.  The result does
+    // not depend on the order spheres are tested in (minimum, ties to the
+    // highest index; or "some occluder").
+    int trips = 0;
     while (true) {
         if (node < B.nnodes && pend == 0) {
             BVH_ST(0, 1);
@@ -305,13 +334,16 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
             }
             node = next;
         }
+        trips++;
         const unsigned long long pm = __builtin_amdgcn_ballot_w64(pend != 0);
         const unsigned long long sm = __builtin_amdgcn_ballot_w64(node < B.nnodes && pend == 0);
         if (pm == 0) {
-            if (sm == 0) break;
+            if (sm == 0 || trips >= RT_BVH_BUDGET) break;
             continue;
         }
-        if (sm != 0 && 64 * __builtin_popcountll(pm) < RT_BVH_BATCH * __builtin_popcountll(pm | sm)) continue;
+        if (sm != 0 && trips < RT_BVH_BUDGET &&
+            64 * __builtin_popcountll(pm) < RT_BVH_BATCH * __builtin_popcountll(pm | sm))
+            continue;
         if (pend != 0) {
             const int f = pend & 0xffffff, c = pend >> 24;
             BVH_ST(1, 1);
@@ -341,12 +373,17 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
             if (!COUNT && shadow && id >= 0) node = B.nnodes;
             pend = 0;
         }
+        if (trips >= RT_BVH_BUDGET) break;
     }
+    W.t = t;
+    W.id = id;
+    W.node = node;
+    W.pend = pend;
 #ifdef RT_BVH_STATS
     {
         const float4 a0 = nodes[0], b0 = nodes[1];
         const bool far = fabsf(r.o.x - a0.x) > b0.x || fabsf(r.o.y - a0.y) > b0.y || fabsf(r.o.z - a0.z) > b0.z;
-        st[7] = st[0] >= 128; st[8] = st[0] >= 512; st[9] = st[0] >= 2048;
+        st[7] = W.node >= B.nnodes && st[0] >= 128; st[8] = st[0] >= 512; st[9] = st[0] >= 2048;
         st[10] = far ? st[0] : 0; st[11] = far; st[12] = shadow; st[13] = shadow ? st[0] : 0;
         st[14] = far && st[0] >= 512;
         st[15] = alpha > 1.f / 128.f; st[16] = st[15] ? st[0] : 0;
@@ -359,7 +396,7 @@ __device__ int query_bvh(const BvhView &B, const ray3 &r, bool shadow, float &t)
     for (int k = 0; k < 21; k++)
         if (st[k]) atomicAdd(&g_bvh_stats[k], (unsigned long long)st[k]);   // divergent: per-lane atomics
 #endif
-    return id;
+    return node >= B.nnodes && pend == 0;
 }
 
 struct Counts { unsigned long long isect, isectp, tests, samples; };
@@ -493,6 +530,8 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         int li = 0;
         int k = 0;
         bool need_cam = nsamples > 0, need_bounce = false;
+        BvhWalk walk;          // GEO_BVH: the current query's walk state
+        bool walking = false;  //   and whether it is suspended mid-walk
         constexpr float nc = 1.f, nt = 1.5f;
 #if RT_SPT_PRIO
         int prio_level = 0, prio_next = nsamples / 4;
@@ -566,7 +605,14 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             int first = -1;
             int id;
             if constexpr (GEO == GEO_BVH) {
-                id = query_bvh<COUNT>(bvh, ray, shadow, t);
+                // Resumable walk: a lane whose query needs more than this
+                // iteration's step budget sits out the rest of the iteration
+                // and continues its walk in the next one.
+                if (!walking) bvh_begin<COUNT>(bvh, ray, shadow, t, walk);
+                walking = !bvh_walk<COUNT>(bvh, ray, shadow, walk);
+                if (walking) continue;
+                t = walk.t;
+                id = walk.id;
                 first = id;                 // any hit: the highest occluder (COUNT)
             } else {
 #if RT_SPT_QV == 2
