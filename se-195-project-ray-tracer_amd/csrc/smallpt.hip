@@ -444,10 +444,14 @@ __device__ __forceinline__ int to_int(float x)
 #ifndef RT_SPT_MINWAVES
 #define RT_SPT_MINWAVES 1   // __launch_bounds__ min waves per SIMD (occupancy A/B builds)
 #endif
+#ifndef RT_BVH_MINWAVES
+#define RT_BVH_MINWAVES 6   // the hierarchy (GEO_BVH) kernels: 93 -> 80 VGPRs (2 spilled), occupancy 5 -> 6: the
+                            // latency-bound walk gains more from the sixth wave than the spills cost (-10 %)
+#endif
 constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2;
 
 template <bool DL, bool COUNT, int GEO>
-__global__ void __launch_bounds__(1024, RT_SPT_MINWAVES)
+__global__ void __launch_bounds__(1024, GEO == 2 ? RT_BVH_MINWAVES : RT_SPT_MINWAVES)
 render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,
               uint32_t *seeds_out, uint32_t *__restrict__ pixels, int w, int h,
