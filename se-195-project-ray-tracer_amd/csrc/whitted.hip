@@ -126,6 +126,10 @@ struct Counts { unsigned long long traced, shadow, tests, tir; };
 // site, so the TRACEDEPTH guards are constant-true).
 // ocl: the device twin of openCLcode.h:150-390 -- a light hit adds the
 // light's colour (openCLcode.h:176-182) instead of (1,1,1); all else equal.
+// COUNT = false: the work counters are dead, so a shadow test stops as soon
+// as every lane of the wave has found an occluder (the reference's own early
+// exit, at wave granularity); only "occluded or not" is used then.
+template <bool COUNT>
 __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &cnt, bool ocl)
 {
     Hit h;
@@ -179,18 +183,23 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
         const float4 lg = S.cen[l];
         const float4 lm = S.mat0[l];
         float shade = 1.0f;
-        if (S.type[l] == SPHERE) {                      // :76-110
-            v3 L = mk(lg.x - pi.x, lg.y - pi.y, lg.z - pi.z);
+        // pi -> light centre, its length and reciprocal: the same float ops
+        // in the shadow test (:76-82) and the shading (:115-125), done once.
+        v3 L = mk(lg.x - pi.x, lg.y - pi.y, lg.z - pi.z);
+        float len, inv;
+        {
             const float d2 = L.x * L.x + L.y * L.y + L.z * L.z;
-            float tdist, inv;
             if (!wave_any(!sqrt_nr_ok(d2))) {
-                tdist = sqrt_nr(d2);
-                inv = rcp_nr(tdist);
+                len = sqrt_nr(d2);
+                inv = rcp_nr(len);
             } else {
-                tdist = sqrt_rn(d2);
-                inv = 1.0f / tdist;
+                len = sqrt_rn(d2);
+                inv = 1.0f / len;
             }
-            L.x *= inv; L.y *= inv; L.z *= inv;
+        }
+        L.x *= inv; L.y *= inv; L.z *= inv;
+        if (S.type[l] == SPHERE) {                      // :76-110
+            const float tdist = len;
             ray3 r;
             r.o = mk(pi.x + L.x * EPS, pi.y + L.y * EPS, pi.z + L.z * EPS);
             r.d = L;
@@ -203,9 +212,11 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
                 int res;
                 const float c = sphere_cand(S.osph[k], r, res);
                 if (res && c < tdist) first = min(first, S.osph_pos[k]);
+                if (!COUNT && !wave_any(first == 0x7fffffff)) break;
             }
 #pragma unroll 4
             for (int k = 0; k < S.nop; k++) {
+                if (!COUNT && !wave_any(first == 0x7fffffff)) break;
                 const float c = plane_cand(S.opln[k], r);
                 if (c < tdist) first = min(first, S.opln_pos[k]);
             }
@@ -213,22 +224,7 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
             cnt.tests += (unsigned long long)(first != 0x7fffffff ? first + 1 : S.nnonlight);
         }
         if (shade > 0) {                                // :112-174
-            v3 L = mk(lg.x, lg.y, lg.z);
-            L.x -= pi.x; L.y -= pi.y; L.z -= pi.z;
-            const float d2 = L.x * L.x + L.y * L.y + L.z * L.z;
-            float len, inv;
-            if (!wave_any(!sqrt_nr_ok(d2))) {
-                len = sqrt_nr(d2);
-                inv = rcp_nr(len);
-            } else {
-                len = sqrt_rn(d2);
-                inv = 1.0f / len;
-            }
-            if (len > 0.0f) {
-                L.x *= inv; L.y *= inv; L.z *= inv;
-            } else {
-                L = mk(0.f, 0.f, 0.f);
-            }
+            if (!(len > 0.0f)) L = mk(0.f, 0.f, 0.f);
             if (pdiff > 0) {
                 float dot = L.x * N.x + L.y * N.y + L.z * N.z;
                 if (dot > 0) {
@@ -521,8 +517,12 @@ __device__ __forceinline__ bool seg_chunk(const WfArgs &A, const SegView &v, int
     return true;
 }
 
+#ifndef RT_WH_MINWAVES
+#define RT_WH_MINWAVES 6    // root/level kernels: occupancy 5 -> 6 (86 -> 79 VGPRs, no spills): -2 %
+#endif
+
 template <bool COUNT>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, RT_WH_MINWAVES)
 root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float *__restrict__ sy_tab,
             float DX, float DY, unsigned long long *__restrict__ counters)
 {
@@ -539,7 +539,7 @@ root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float
         Hit hh;
         bool tir = false;
         if (active) {
-            hh = trace(S, primary(sub, SX, SY, DX, DY, A.side), 1.0f, cnt, A.ocl);
+            hh = trace<COUNT>(S, primary(sub, SX, SY, DX, DY, A.side), 1.0f, cnt, A.ocl);
             tir = hh.refr > 0 && !hh.refr_ray_ok;
             if (tir) cnt.tir++;
         }
@@ -561,7 +561,7 @@ root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float
 // Level L = 1..5: a grid of resident blocks; wave w takes 64-ray chunks
 // w, w + #waves, ... of the level's queue.
 template <bool COUNT>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, RT_WH_MINWAVES)
 level_kernel(WfArgs A, int L, unsigned long long *__restrict__ counters)
 {
     __shared__ Scene S;
@@ -584,7 +584,7 @@ level_kernel(WfArgs A, int L, unsigned long long *__restrict__ counters)
             r.o = mk(a.x, a.y, a.z);
             r.d = mk(a.w, b.x, b.y);
             tree = __float_as_int(b.w);
-            hh = trace(S, r, b.z, cnt, A.ocl);
+            hh = trace<COUNT>(S, r, b.z, cnt, A.ocl);
             tir = hh.refr > 0 && !hh.refr_ray_ok;
             if (tir && L < 5) cnt.tir++;                // node index < 31 (:398)
             A.lcol[L][q] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
@@ -803,7 +803,7 @@ fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict
                 }
             }
             Counts c1 = {0, 0, 0, 0};
-            Hit hh = trace(S, r, rin, c1, A.ocl);
+            Hit hh = trace<COUNT>(S, r, rin, c1, A.ocl);
             const bool tir = hh.refr > 0 && !hh.refr_ray_ok;
             if (wf < 0) {                  // not traced by the level pass: count it here
                 cnt.traced += c1.traced; cnt.shadow += c1.shadow; cnt.tests += c1.tests;
