@@ -394,6 +394,8 @@ struct WfArgs {
     const Scene *scene;       // scene image (scene_kernel)
     float4 *rcol;             // [ntrees] root colour.xyz, dist
     int *rinfo;               // [ntrees] hit primitive | INFO_*
+    float4 *psum;             // [npix] sum (xyz) of the colours of the pixel's leading childless trees,
+                              //   in sub-sample order, and (w, int bits) the first sub-sample not in it
     int2 *rchild;             // [ntrees] queue slots (level 1) of refl / refr child, -1 if none
     int *fixflag;             // [ntrees] 0, or -1 once queued for fixup
     int *fixlist;             // [ntrees] trees to fix
@@ -535,6 +537,13 @@ root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float
     const int pix = (y - A.row_begin) * A.w + x;
     const float SX = active ? sx_tab[x] : 0.f, SY = active ? sy_tab[y] : 0.f;
     Counts cnt = {0, 0, 0, 0};
+    // A tree without children (a plane, a light, a miss) is final at its
+    // root: while the pixel's trees are childless their colours are summed
+    // here, in sub-sample order with the same float adds as final_kernel
+    // (:513-515), and only the trees from the first one with children on
+    // are recorded for the later passes.
+    float tr = 0.f, tg = 0.f, tb = 0.f;
+    int kfirst = A.nsub;
     for (int sub = 0; sub < A.nsub; sub++) {
         Hit hh;
         bool tir = false;
@@ -547,11 +556,17 @@ root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float
         const int wave_id = ((blockIdx.y * gridDim.x + blockIdx.x) << 2) + wave;
         const int2 ch = queue_children(A, 0, wave_id, active, tree, tree, 0, hh, tir);
         if (active) {
-            A.rcol[tree] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
-            A.rinfo[tree] = node_info(hh, tir);
-            A.rchild[tree] = ch;
+            if (kfirst == A.nsub && !(hh.refl > 0 || hh.refr > 0)) {
+                tr += hh.acc.x; tg += hh.acc.y; tb += hh.acc.z;
+            } else {
+                if (kfirst == A.nsub) kfirst = sub;
+                A.rcol[tree] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
+                A.rinfo[tree] = node_info(hh, tir);
+                A.rchild[tree] = ch;
+            }
         }
     }
+    if (active) A.psum[pix] = make_float4(tr, tg, tb, __int_as_float(kfirst));
     if (COUNT) {
         const unsigned long long c[4] = {cnt.traced, cnt.shadow, cnt.tests, cnt.tir};
         flush_counters<4>(counters, c);
@@ -728,8 +743,9 @@ final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
     const int y = A.row_begin + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
     if (x >= A.w || y >= row_end) return;
     const int pix = (y - A.row_begin) * A.w + x;
-    float tr = 0.f, tg = 0.f, tb = 0.f;
-    for (int sub = 0; sub < A.nsub; sub++) {
+    const float4 ps = A.psum[pix];                          // the leading childless trees, summed by root_kernel
+    float tr = ps.x, tg = ps.y, tb = ps.z;
+    for (int sub = __float_as_int(ps.w); sub < A.nsub; sub++) {
         const int tree = sub * A.npix + pix;
         float4 c0 = A.rcol[tree];
         if (A.fixflag[tree] == 0) {
@@ -947,7 +963,7 @@ int wavefront_arena(rtrt::DeviceState &st, int w, int rows, int nsub, rt::whitte
     C = SC * NSEG;
     const size_t TC = std::max<size_t>(C / 8, 1024);    // TIR list per level
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t root_b = al(T * 16) + al(T * 4) + al(T * 8) + al(T * 4) + al(T * 4);
+    const size_t root_b = al(T * 16) + al(T * 4) + al((size_t)w * rows * 16) + al(T * 8) + al(T * 4) + al(T * 4);
     const size_t lvl_b = al(C * 16) * 3 + al(C * 4) * 2 + al(C * 8) + al(TC * 16);
     const size_t bytes = al(sizeof(Scene)) + root_b + LEVELS * lvl_b + al(sizeof(int) * C_TOTAL * CSTRIDE);
     void *base = nullptr;
@@ -958,6 +974,7 @@ int wavefront_arena(rtrt::DeviceState &st, int w, int rows, int nsub, rt::whitte
     A->scene = (const Scene *)take(sizeof(Scene));
     A->rcol = (float4 *)take(T * 16);
     A->rinfo = (int *)take(T * 4);
+    A->psum = (float4 *)take((size_t)w * rows * 16);
     A->rchild = (int2 *)take(T * 8);
     A->fixflag = (int *)take(T * 4);
     A->fixlist = (int *)take(T * 4);
