@@ -211,6 +211,9 @@ constexpr float BVH_ALPHA_R = 1.f / 64.f;   // per node, with BETA, in the node 
 #ifndef RT_BVH_BATCH
 #define RT_BVH_BATCH 32     // leaf postponement: test pending leaves once >= BATCH/64 of the walking lanes hold one
 #endif
+#ifndef RT_BVH_LEAF_BF
+#define RT_BVH_LEAF_BF 1    // branch-free leaf sphere tests (configs[4] 40.5 -> 39.5 ms; 0 = per-sphere branch, A/B)
+#endif
 #ifndef RT_BVH_BUDGET
 #define RT_BVH_BUDGET 32    // walk steps per render-loop iteration before a lane's query is suspended
 #endif
@@ -357,6 +360,40 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
                 g[q] = B.geo[j];
                 gi[q] = B.id[j];
             }
+#if RT_BVH_LEAF_BF
+            // Branch-free sphere tests (as query_bf): sqrt_nr is exact for det
+            // in [2^-96, inf) and NaN below 0 (a miss); a wave with a lane
+            // meeting 0 <= |det| < 2^-96 redoes the leaf with sphere_hit.
+            float dq[BVH_LEAF_MAX];
+            bool bad = false;
+#pragma unroll
+            for (int q = 0; q < BVH_LEAF_MAX; q++) {
+                const float opx = g[q].x - r.o.x, opy = g[q].y - r.o.y, opz = g[q].z - r.o.z;
+                const float bb = opx * r.d.x + opy * r.d.y + opz * r.d.z;
+                const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g[q].w;
+                bad = bad || (q < c && fabsf(det) < 0x1p-96f);
+                const float sd = sqrt_nr(det);
+                const float t1 = bb - sd, t2 = bb + sd;
+                dq[q] = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
+            }
+            if (wave_any(bad)) {
+#pragma unroll
+                for (int q = 0; q < BVH_LEAF_MAX; q++) dq[q] = sphere_hit(g[q], r);
+            }
+#pragma unroll
+            for (int q = 0; q < BVH_LEAF_MAX; q++) {
+                if (q < c) {
+                    const float d = dq[q];
+                    const int i = gi[q];
+                    if (shadow) {
+                        if (d < maxt && i > id) id = i;
+                    } else if (d < t || (d == t && i > id)) {
+                        t = d;
+                        id = i;
+                    }
+                }
+            }
+#else
 #pragma unroll
             for (int q = 0; q < BVH_LEAF_MAX; q++) {
                 if (q < c) {
@@ -370,6 +407,7 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
                     }
                 }
             }
+#endif
             if (!COUNT && shadow && id >= 0) node = B.nnodes;
             pend = 0;
         }
