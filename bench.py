@@ -97,10 +97,46 @@ def cpu_baseline(args):
                          row_end=r0 + rows2, nthreads=threads)
     dt = time.perf_counter() - t0
     rays = c[0] + c[1]
-    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": "oracle/smallpt_oracle.c, rows [%d,%d) of the 1920x1080 Cornell frame at 64 spp "
-                      "(%d samples, %.1f s, %d threads; %.3f Msamples/s)"
-                      % (r0, r0 + rows2, c[3], dt, threads, c[3] / dt / 1e6)}
+    out = {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+           "sample": "oracle/smallpt_oracle.c, rows [%d,%d) of the 1920x1080 Cornell frame at 64 spp "
+                     "(%d samples, %.1f s, %d threads; %.3f Msamples/s)"
+                     % (r0, r0 + rows2, c[3], dt, threads, c[3] / dt / 1e6),
+           "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
+    # The reference's own code (oracle/_ref: RadiancePathTracing & co. of
+    # smallptgpu-v1.6 compiled from its sources) on one thread, as the
+    # reference's CPU path runs; rays counted by the port on the same band
+    # (identical work, checked bit for bit in tests/test_oracle.py).
+    refs = O.ref_libs()
+    if refs is not None:
+        RS = refs[1]
+        rows3, dt3 = 2, 0.0
+        for _ in range(2):                  # probe, then a band sized to ~3 s
+            if dt3:
+                rows3 = int(min(H, max(rows3, rows3 * 3.0 / max(dt3, 1e-3))))
+            r3 = H // 2 - rows3 // 2
+            sd = seeds.copy()
+            t0 = time.perf_counter()
+            RS.ref_smallpt_render(S, n, C.byref(cam), col.ctypes.data, sd.ctypes.data, px.ctypes.data,
+                                  W, H, r3, r3 + rows3, 0, SPP, 0)
+            dt3 = time.perf_counter() - t0
+        c3 = O.smallpt_render(S, n, cam, col, seeds.copy(), px, W, H, 0, SPP, row_begin=r3,
+                              row_end=r3 + rows3, nthreads=threads)
+        out["reference_1thread"] = {
+            "value": round((c3[0] + c3[1]) / dt3 / 1e6, 3), "unit": "Mrays/s", "cores": 1, "kind": "reference",
+            "sample": "oracle/_ref/libref_smallpt.so (the reference's geomfunc.h radiance), rows [%d,%d) of "
+                      "the same frame at 64 spp, %.1f s, one thread" % (r3, r3 + rows3, dt3)}
+    return out
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def whitted_line(args, dev):
