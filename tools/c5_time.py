@@ -48,7 +48,7 @@ if stats:
     print("  queries >= 128/512/2048 nodes: %d %d %d of %d; origin outside root box: %d queries, %.1f nodes each, "
           "%d of them >= 512; shadow: %d queries, %.1f nodes each" % (
               bs[7], bs[8], bs[9], bs[5], bs[11], bs[10] / max(bs[11], 1), bs[14], bs[12], bs[13] / max(bs[12], 1)))
-    print("  alpha != 1/128: %d queries, %.1f nodes each, %d >= 512; origin > 8 root radii away: %d queries, "
+    print("  alpha > 1/128: %d queries, %.1f nodes each, %d >= 512; origin > 8 root radii away: %d queries, "
           "%.1f nodes each, %d >= 512" % (bs[15], bs[16] / max(bs[15], 1), bs[20], bs[17], bs[18] / max(bs[17], 1), bs[19]))
 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 a.record(st)
