@@ -152,6 +152,67 @@ int spt_scene_render_async(const spt_scene *scene, const rt_camera *camera, floa
 int spt_pack_pixels_async(const float *d_colors, uint32_t *d_pixels, int w, int h, int row_begin,
                           int row_end, void *stream);
 
+/* ------------------------------------------------------------ smallpt, several GPUs */
+/* One frame tiled over the GPUs of a node in row bands:
+ * band k owns the k-th contiguous chunk of the flipped colour / seed slots,
+ * i.e. pixel rows [h - e_k, h - s_k) with s_k = k*h/ngpus, e_k = (k+1)*h/ngpus.
+ * Every pixel keeps its RNG words and accumulator on its band's device, so
+ * rendering needs no exchange; samples of a pixel are never split.  One host
+ * thread drives all devices (one stream each), as the reference's single
+ * host thread drove its one OpenCL queue (smallptGPU.cpp:617-640,739-760).
+ *
+ * devices: ngpus device ordinals (NULL: 0..ngpus-1).  A device may repeat
+ * (several bands on one GPU -- the same band/assemble code on one device).
+ * Each band holds a full-frame colour / seed / pixel array on its device;
+ * only its own rows are authoritative until spt_multi_gather_async. */
+typedef struct spt_multi spt_multi;
+int spt_multi_create(const rt_sphere *spheres, unsigned nspheres, int w, int h, const int *devices,
+                     int ngpus, spt_multi **out);
+int spt_multi_destroy(spt_multi *m);
+/* Re-uploads the scene to every band's device (ReInitSceneGPU). */
+int spt_multi_set_scene(spt_multi *m, const rt_sphere *spheres, unsigned nspheres);
+/* Pixel-row bounds: rows[k] .. rows[k+1] hold band k's rows in FLIPPED
+ * order, i.e. band k renders pixel rows [h - rows[k+1], h - rows[k]).
+ * rows: ngpus + 1 ints. */
+int spt_multi_bands(const spt_multi *m, int *rows);
+/* Host -> bands: each band's rows of seeds (2*w*h words, flipped slots) and,
+ * when colors is not NULL, of the accumulator (3*w*h floats).  Blocking. */
+int spt_multi_upload(spt_multi *m, const float *colors, const uint32_t *seeds);
+/* Samples first_sample .. first_sample+nsamples-1 of every pixel, each band
+ * on its own device, asynchronous.  counters: accumulate the four
+ * spt_render counters (read with spt_multi_counters). */
+int spt_multi_render_async(spt_multi *m, const rt_camera *camera, int first_sample, int nsamples,
+                           int mode, int counters);
+/* Assembles the whole HDR accumulator on every band's device and repacks
+ * each device's RGBA8 frame from it (spt_pack_pixels_async).  Distinct
+ * devices: one RCCL group (ncclGroupStart / one ncclBroadcast per band /
+ * ncclGroupEnd) over xGMI; repeated devices or RT_SPT_GATHER=peer: stream-
+ * ordered peer copies (RT_SPT_GATHER=rccl runs the RCCL group even for a
+ * single band).  Asynchronous. */
+int spt_multi_gather_async(spt_multi *m);
+/* Waits for every band's device work. */
+int spt_multi_sync(spt_multi *m);
+/* Bands -> host, blocking: each band's rows of colors / seeds / pixels
+ * (each nullable) -- the assembled frame, no collective needed. */
+int spt_multi_download(spt_multi *m, float *colors, uint32_t *seeds, uint32_t *pixels);
+/* Band k's whole device frame -> host, blocking (after a gather: the
+ * assembled frame as band k's device holds it).  Either pointer nullable. */
+int spt_multi_read_frame(spt_multi *m, int k, float *colors, uint32_t *pixels);
+/* Sums the per-band counters into out[4] (blocking) and zeroes them. */
+int spt_multi_counters(spt_multi *m, uint64_t *out);
+/* Band k's device frame and stream (after a gather: the whole frame). */
+int spt_multi_band_buffers(const spt_multi *m, int k, int *device, float **d_colors, uint32_t **d_seeds,
+                           uint32_t **d_pixels, void **stream);
+
+/* spt_render over several GPUs (SURVEY.md §8(b) "spt_render(..., ngpus)"):
+ * the same contract and results as spt_render, the frame tiled in row bands
+ * over devices[0..ngpus-1] (NULL: 0..ngpus-1), host buffers assembled band
+ * by band.  Blocking. */
+int spt_render_multi(const rt_sphere *spheres, unsigned nspheres, const rt_camera *camera,
+                     float *colors, uint32_t *seeds, uint32_t *pixels, int w, int h,
+                     int first_sample, int nsamples, int mode, uint64_t *counters,
+                     const int *devices, int ngpus);
+
 /* Host helper: AllocateBuffers' seed fill (smallptGPU.cpp:105-110) --
  * srand(seed); seeds[i] = max(rand(), 2) for i < n, with the host libc's
  * rand() (glibc on the reference's Linux build). */

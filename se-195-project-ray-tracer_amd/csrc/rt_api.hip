@@ -105,6 +105,24 @@ int scratch(DeviceState &st, int slot, size_t bytes, void **out)
     return RT_OK;
 }
 
+int thread_device() { return g_dev; }
+
+DeviceScope::DeviceScope() : saved_rt(g_dev) { (void)hipGetDevice(&saved_hip); }
+
+DeviceScope::~DeviceScope()
+{
+    g_dev = saved_rt;
+    (void)hipSetDevice(saved_hip);
+}
+
+int DeviceScope::select(int device)
+{
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
+    g_dev = device;
+    return RT_OK;
+}
+
 }  // namespace rtrt
 
 extern "C" const char *rt_last_error(void) { return rtrt::g_err; }

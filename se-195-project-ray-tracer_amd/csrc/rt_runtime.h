@@ -36,6 +36,17 @@ int check_launch(const char *what);
 int state(DeviceState **out);
 // Device buffer slot `slot` of at least `bytes` (grow-only, reused).
 int scratch(DeviceState &st, int slot, size_t bytes, void **out);
+// The calling thread's rt_set_device choice (-1: none, HIP's current device).
+int thread_device();
+// Saves the calling thread's device selection (rt_set_device and HIP's
+// current device) and restores both on scope exit: the multi-device entry
+// points drive several devices from one host thread.
+struct DeviceScope {
+    int saved_rt, saved_hip = 0;
+    DeviceScope();
+    ~DeviceScope();
+    int select(int device);   // rt_set_device for the scope's duration
+};
 
 }  // namespace rtrt
 

@@ -12,11 +12,15 @@
 // Where rendering_kernel.cl computed a different image (seed slot = gid,
 // OpenCL sign(0) = 0, clang argument order: SURVEY.md §8(a) S10), the HIP
 // path computes the CPU path's (UpdateRenderingCPU, smallptCPU.cpp:77-132).
-// Buffers stay device-resident across passes; only the RGBA8 frame is read
-// back per UpdateRenderingGPU call, as clEnqueueReadBuffer did (:760).
+// Frames are tiled in row bands over every visible gfx950 GPU (spt_multi:
+// each pixel's accumulator and RNG words live on its band's device, so a pass
+// needs no exchange); buffers stay device-resident across passes and only
+// the RGBA8 frame is read back per UpdateRenderingGPU call, band by band, as
+// clEnqueueReadBuffer did (:760).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <vector>
 
 #include <hip/hip_runtime.h>
 #include "../../include/rt_hip.h"
@@ -37,11 +41,11 @@ extern void UpdateCamera();            // displayfunc.cpp:182-195
 extern double WallClockTime();         // displayfunc.cpp:69-80
 
 namespace {
-spt_scene *scene = nullptr;
-float *d_colors = nullptr;
-uint32_t *d_seeds = nullptr, *d_pixels = nullptr;
+// The frame, tiled in row bands over every GPU the shim drives (one band on
+// a one-GPU node); accumulators and RNG words stay on their band's device.
+spt_multi *frame = nullptr;
+std::vector<int> devices;
 uint32_t *h_seeds = nullptr;
-hipStream_t stream = nullptr;
 
 void die(const char *what, int rc)
 {
@@ -49,28 +53,42 @@ void die(const char *what, int rc)
     exit(-1);
 }
 
-void die_hip(const char *what, hipError_t e)
+// The devices to tile frames over: RT_SPT_DEVICES="0,1,..." (a device may
+// repeat: several bands on one GPU), else every visible gfx950 GPU, at most
+// RT_SPT_GPUS of them.  (The reference picks one OpenCL device,
+// smallptGPU.cpp:225-300.)
+void pick_devices()
 {
-    fprintf(stderr, "%s: %s (%d)\n", what, hipGetErrorString(e), (int)e);
-    exit(-1);
-}
-
-void upload_scene()
-{
-    if (scene) spt_scene_destroy(scene);
-    scene = nullptr;
-    int rc = spt_scene_create(spheres, sphereCount, &scene);
-    if (rc) die("Failed to write the HIP scene buffer", rc);
+    devices.clear();
+    if (const char *e = getenv("RT_SPT_DEVICES")) {
+        for (const char *p = e; *p;) {
+            char *end;
+            const long d = strtol(p, &end, 10);
+            if (end == p) break;
+            devices.push_back((int)d);
+            p = *end == ',' ? end + 1 : end;
+        }
+    } else {
+        const int n = rt_device_count();
+        int cap = n;
+        if (const char *g = getenv("RT_SPT_GPUS")) cap = atoi(g) > 0 ? atoi(g) : n;
+        for (int d = 0; d < n && (int)devices.size() < cap; d++) {
+            hipDeviceProp_t prop;
+            if (hipGetDeviceProperties(&prop, d) == hipSuccess && !strncmp(prop.gcnArchName, "gfx950", 6))
+                devices.push_back(d);
+        }
+    }
+    if (devices.empty()) {
+        fprintf(stderr, "Failed to find a gfx950 HIP device: %s\n", rt_last_error());
+        exit(-1);
+    }
 }
 
 // FreeBuffers (smallptGPU.cpp:76-98)
 void FreeBuffers()
 {
-    if (d_colors) (void)hipFree(d_colors);
-    if (d_seeds) (void)hipFree(d_seeds);
-    if (d_pixels) (void)hipFree(d_pixels);
-    d_colors = nullptr;
-    d_seeds = d_pixels = nullptr;
+    if (frame) spt_multi_destroy(frame);
+    frame = nullptr;
     free(h_seeds);
     free(pixels);
     h_seeds = nullptr;
@@ -78,7 +96,8 @@ void FreeBuffers()
 }
 
 // AllocateBuffers (smallptGPU.cpp:100-167): seeds from rand() (>= 2),
-// pixels preset to their index ("Test colors", :111-113), device buffers.
+// pixels preset to their index ("Test colors", :111-113), device buffers
+// (scene, accumulator, seeds, pixels) on every band's device.
 void AllocateBuffers()
 {
     const int pixelCount = width * height;
@@ -89,37 +108,35 @@ void AllocateBuffers()
     }
     pixels = (unsigned int *)malloc(sizeof(unsigned int) * pixelCount);
     for (int i = 0; i < pixelCount; ++i) pixels[i] = i;
-    hipError_t e = hipMalloc(&d_colors, sizeof(float) * 3 * pixelCount);
-    if (e != hipSuccess) die_hip("Failed to create HIP output buffer", e);
-    e = hipMalloc(&d_pixels, sizeof(uint32_t) * pixelCount);
-    if (e != hipSuccess) die_hip("Failed to create HIP pixel buffer", e);
-    e = hipMalloc(&d_seeds, sizeof(uint32_t) * pixelCount * 2);
-    if (e != hipSuccess) die_hip("Failed to create HIP seed buffer", e);
-    e = hipMemcpy(d_seeds, h_seeds, sizeof(uint32_t) * pixelCount * 2, hipMemcpyHostToDevice);
-    if (e != hipSuccess) die_hip("Failed to write the HIP seeds buffer", e);
+    int rc = spt_multi_create(spheres, sphereCount, width, height, devices.data(), (int)devices.size(), &frame);
+    if (rc) die("Failed to create HIP buffers", rc);
+    rc = spt_multi_upload(frame, nullptr, h_seeds);
+    if (rc) die("Failed to write the HIP seeds buffer", rc);
 }
 
-// ExecuteKernel (smallptGPU.cpp:617-640): one pass = one sample per pixel.
+// ExecuteKernel (smallptGPU.cpp:617-640): one pass = one sample per pixel,
+// every band on its own device.
 void ExecuteKernel()
 {
-    int rc = spt_scene_render_async(scene, &camera, d_colors, d_seeds, d_seeds, d_pixels, width, height, 0,
-                                    height, currentSample, 1, smallptHipMode, nullptr, stream);
+    int rc = spt_multi_render_async(frame, &camera, currentSample, 1, smallptHipMode, 0);
     if (rc) die("Failed to enqueue HIP work", rc);
+}
+
+void Finish()                          // clFinish (smallptGPU.cpp:748)
+{
+    int rc = spt_multi_sync(frame);
+    if (rc) die("Failed to finish HIP work", rc);
 }
 }  // namespace
 
-// SetUpOpenCL (smallptGPU.cpp:209-615): device, stream, scene and buffers.
+// SetUpOpenCL (smallptGPU.cpp:209-615): devices, scene and buffers.
 void SetUpHIP()
 {
     if (rt_device_count() < 1) {
         fprintf(stderr, "Failed to find a HIP device: %s\n", rt_last_error());
         exit(-1);
     }
-    int rc = rt_set_device(0);
-    if (rc) die("Failed to select HIP device 0", rc);
-    hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
-    if (e != hipSuccess) die_hip("Failed to create HIP stream", e);
-    upload_scene();
+    pick_devices();
     AllocateBuffers();
 }
 
@@ -139,17 +156,14 @@ void UpdateRenderingGPU()
         const float tresholdTime = 0.5f * k;
         for (;;) {
             ExecuteKernel();
-            hipError_t e = hipStreamSynchronize(stream);
-            if (e != hipSuccess) die_hip("Failed to finish HIP work", e);
+            Finish();
             currentSample++;
             const float elapsedTime = WallClockTime() - startTime;
             if (elapsedTime > tresholdTime) break;
         }
     }
-    hipError_t e = hipMemcpyAsync(pixels, d_pixels, sizeof(unsigned int) * width * height,
-                                  hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(stream);
-    if (e != hipSuccess) die_hip("Failed to read the HIP pixel buffer", e);
+    int rc = spt_multi_download(frame, nullptr, nullptr, pixels);   // every band's rows
+    if (rc) die("Failed to read the HIP pixel buffer", rc);
     const double elapsedTime = WallClockTime() - startTime;
     const int samples = currentSample - startSampleCount;
     const double sampleSec = samples * height * width / elapsedTime;
@@ -161,7 +175,8 @@ void UpdateRenderingGPU()
 void ReInitSceneGPU()
 {
     currentSample = 0;
-    upload_scene();
+    int rc = spt_multi_set_scene(frame, spheres, sphereCount);
+    if (rc) die("Failed to write the HIP scene buffer", rc);
 }
 
 // ReInitGPU (smallptGPU.cpp:805-830).  The camera travels by value with every
@@ -181,9 +196,12 @@ void ReInitGPU(const int reallocBuffers)
 // Test / tooling hook: the device HDR accumulator (Vec per flipped slot).
 void SmallptHipReadColors(float *out)
 {
-    hipError_t e = hipMemcpy(out, d_colors, sizeof(float) * 3 * width * height, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) die_hip("Failed to read the HIP colour buffer", e);
+    int rc = spt_multi_download(frame, out, nullptr, nullptr);
+    if (rc) die("Failed to read the HIP colour buffer", rc);
 }
 
 // Test / tooling hook: the seeds AllocateBuffers drew (host copy, 2*W*H).
 const unsigned int *SmallptHipInitialSeeds() { return h_seeds; }
+
+// Test / tooling hook: the number of row bands (GPUs) frames are tiled over.
+int SmallptHipBands() { return (int)devices.size(); }

@@ -102,7 +102,7 @@ char *openCLcode()
     outputLine2 = "2: compute units: " + std::to_string(prop.multiProcessorCount);
     outputLine3 = "3: global memory: " + std::to_string(prop.totalGlobalMem >> 20) + " MB";
     outputLine4 = "4: LDS per block: " + std::to_string(prop.sharedMemPerBlock) + " B";
-    outputLine5 = "5: kernel: rt::whitted::render_kernel (gfx950)";
+    outputLine5 = "5: kernels: rt::whitted::root/level/tir/backacc/final_kernel (gfx950)";
     outputLine6 = "6: useGPU = " + std::to_string(useGPU);
     return strdup(outputLine1.c_str());
 }

@@ -7,7 +7,9 @@ what the tests, bench.py and __graft_entry__ drive.
     Whitted  : whitted_render()  ~ Engine_InitRender + Engine_Render
                (raytracer3.0.06.no_rec.samp/raytracer.cpp:278-530) on the GPU
     smallpt  : SmallptFrame.render(k)  ~ k x UpdateRenderingCPU
-               (smallptgpu-v1.6/smallptCPU.cpp:77-132) on the GPU
+               (smallptgpu-v1.6/smallptCPU.cpp:77-132) on the GPU, or
+               tiled in row bands over several GPUs (devices=[...]);
+               SmallptMulti: the device-resident multi-GPU frame (spt_multi_*)
 """
 import ctypes as C
 
@@ -18,7 +20,7 @@ from ._lib import (Camera, Primitive, RTError, Sphere, Vec3, check, device_count
                    set_device, SPT_DIRECT_LIGHTING, SPT_PATH_TRACING)
 
 __all__ = ["Camera", "Primitive", "Sphere", "Vec3", "RTError", "scenes", "lib", "check",
-           "device_count", "set_device", "whitted_render", "SmallptFrame", "SmallptScene",
+           "device_count", "set_device", "whitted_render", "SmallptFrame", "SmallptScene", "SmallptMulti",
            "SPT_PATH_TRACING", "SPT_DIRECT_LIGHTING"]
 
 
@@ -72,15 +74,21 @@ class SmallptFrame:
         self.current_sample = 0
         self.counters = [0, 0, 0, 0]
 
-    def render(self, nsamples=1, counters=True):
+    def render(self, nsamples=1, counters=True, devices=None):
         """nsamples successive UpdateRenderingCPU passes on the GPU.  With
         counters=False no counter buffer is passed (the kernels without the
-        work counters: the ones bench.py times)."""
+        work counters: the ones bench.py times).  devices=[d0, d1, ...]: the
+        frame tiled in row bands over those devices (spt_render_multi; a
+        device may repeat)."""
         cnt = (C.c_uint64 * 4)()
-        check(lib().spt_render(C.addressof(self.spheres), self.nspheres, C.byref(self.camera),
-                               self.colors.ctypes.data, self.seeds.ctypes.data,
-                               self.pixels.ctypes.data, self.w, self.h, self.current_sample,
-                               nsamples, self.mode, C.addressof(cnt) if counters else None))
+        args = (C.addressof(self.spheres), self.nspheres, C.byref(self.camera), self.colors.ctypes.data,
+                self.seeds.ctypes.data, self.pixels.ctypes.data, self.w, self.h, self.current_sample,
+                nsamples, self.mode, C.addressof(cnt) if counters else None)
+        if devices is None:
+            check(lib().spt_render(*args))
+        else:
+            devs = (C.c_int * len(devices))(*devices)
+            check(lib().spt_render_multi(*args, devs, len(devices)))
         self.current_sample += nsamples
         self.counters = [a + b for a, b in zip(self.counters, cnt)]
         return self
@@ -98,6 +106,76 @@ class SmallptScene:
     def close(self):
         if self.handle:
             lib().spt_scene_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SmallptMulti:
+    """A frame tiled in row bands over several devices (spt_multi_*): band k
+    renders pixel rows [h - rows[k+1], h - rows[k]) on devices[k]; gather()
+    assembles the whole frame on every band's device (RCCL group of
+    broadcasts, or peer copies when a device repeats)."""
+
+    def __init__(self, w, h, devices, spheres=None, nspheres=None):
+        if spheres is None:
+            spheres, nspheres = scenes.cornell()
+        self.w, self.h, self.devices = w, h, list(devices)
+        self.handle = C.c_void_p()
+        devs = (C.c_int * len(self.devices))(*self.devices)
+        check(lib().spt_multi_create(C.addressof(spheres), nspheres, w, h, devs, len(self.devices),
+                                     C.byref(self.handle)))
+        rows = (C.c_int * (len(self.devices) + 1))()
+        check(lib().spt_multi_bands(self.handle, rows))
+        self.rows = list(rows)
+
+    def set_scene(self, spheres, nspheres):
+        check(lib().spt_multi_set_scene(self.handle, C.addressof(spheres), nspheres))
+
+    def upload(self, seeds, colors=None):
+        check(lib().spt_multi_upload(self.handle, colors.ctypes.data if colors is not None else None,
+                                     seeds.ctypes.data))
+
+    def render(self, camera, first_sample, nsamples, mode=SPT_PATH_TRACING, counters=False):
+        check(lib().spt_multi_render_async(self.handle, C.byref(camera), first_sample, nsamples, mode,
+                                           int(bool(counters))))
+
+    def gather(self):
+        check(lib().spt_multi_gather_async(self.handle))
+
+    def sync(self):
+        check(lib().spt_multi_sync(self.handle))
+
+    def download(self, colors=None, seeds=None, pixels=None):
+        ptr = lambda a: a.ctypes.data if a is not None else None  # noqa: E731
+        check(lib().spt_multi_download(self.handle, ptr(colors), ptr(seeds), ptr(pixels)))
+
+    def read_frame(self, k):
+        """Band k's whole device frame: (colors float32[3*w*h], pixels uint32[w*h])."""
+        col = np.empty(3 * self.w * self.h, np.float32)
+        px = np.empty(self.w * self.h, np.uint32)
+        check(lib().spt_multi_read_frame(self.handle, k, col.ctypes.data, px.ctypes.data))
+        return col, px
+
+    def counters(self):
+        out = (C.c_uint64 * 4)()
+        check(lib().spt_multi_counters(self.handle, out))
+        return list(out)
+
+    def band_buffers(self, k):
+        """(device, d_colors, d_seeds, d_pixels, stream) of band k."""
+        dev = C.c_int()
+        p = [C.c_void_p() for _ in range(4)]
+        check(lib().spt_multi_band_buffers(self.handle, k, C.byref(dev), *[C.byref(x) for x in p]))
+        return (dev.value,) + tuple(x.value for x in p)
+
+    def close(self):
+        if self.handle:
+            lib().spt_multi_destroy(self.handle)
             self.handle = C.c_void_p()
 
     def __del__(self):

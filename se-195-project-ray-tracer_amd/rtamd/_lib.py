@@ -17,7 +17,10 @@ SPT_PATH_TRACING, SPT_DIRECT_LIGHTING = 0, 1
 # Every symbol include/rt_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = ("rt_last_error", "rt_device_count", "rt_set_device", "rt_release", "rt_cached_bytes",
            "rtw_render", "rtw_render_async", "rtw_render_ocl", "rtw_render_ocl_async", "spt_render", "spt_render_async", "spt_seed_fill",
-           "spt_scene_create", "spt_scene_destroy", "spt_scene_render_async", "spt_pack_pixels_async")
+           "spt_scene_create", "spt_scene_destroy", "spt_scene_render_async", "spt_pack_pixels_async",
+           "spt_multi_create", "spt_multi_destroy", "spt_multi_set_scene", "spt_multi_bands", "spt_multi_upload",
+           "spt_multi_render_async", "spt_multi_gather_async", "spt_multi_sync", "spt_multi_download",
+           "spt_multi_read_frame", "spt_multi_counters", "spt_multi_band_buffers", "spt_render_multi")
 
 
 class RTError(RuntimeError):
@@ -81,6 +84,22 @@ def lib():
     if hasattr(L, "spt_pack_pixels_async"):   # (absent from older A/B builds under RT_HIP_LIB)
         L.spt_pack_pixels_async.argtypes = [vp, vp, i, i, i, i, vp]
     L.spt_seed_fill.restype = None
+    if hasattr(L, "spt_multi_create"):
+        ip = C.POINTER(C.c_int)
+        L.spt_multi_create.argtypes = [vp, u, i, i, vp, i, C.POINTER(vp)]
+        L.spt_multi_destroy.argtypes = [vp]
+        L.spt_multi_set_scene.argtypes = [vp, vp, u]
+        L.spt_multi_bands.argtypes = [vp, vp]
+        L.spt_multi_upload.argtypes = [vp, vp, vp]
+        L.spt_multi_render_async.argtypes = [vp, vp, i, i, i, i]
+        L.spt_multi_gather_async.argtypes = [vp]
+        L.spt_multi_sync.argtypes = [vp]
+        L.spt_multi_download.argtypes = [vp, vp, vp, vp]
+        L.spt_multi_read_frame.argtypes = [vp, i, vp, vp]
+        L.spt_multi_counters.argtypes = [vp, vp]
+        L.spt_multi_band_buffers.argtypes = [vp, i, ip, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp),
+                                             C.POINTER(vp)]
+        L.spt_render_multi.argtypes = [vp, u, vp, vp, vp, vp, i, i, i, i, i, u64p, vp, i]
     _lib = L
     return L
 

@@ -2,11 +2,17 @@
 // the idle loop (displayfunc.cpp:197-204 -> UpdateRenderingGPU) over the HIP
 // drop-in shim (csrc/shim_smallpt.cpp).  UpdateCamera is the oracle's
 // restatement (test infrastructure).  Runs argv[3] UpdateRenderingGPU calls
-// and writes pixels (W*H u32), the device HDR colours (3*W*H f32) the
-// initial seeds AllocateBuffers drew and currentSample to argv[4].
+// -- or, with argv[5], a script of comma-separated steps: "pN" N
+// UpdateRenderingGPU calls, "R" ReInitGPU(1) (FreeBuffers + AllocateBuffers:
+// fresh rand() seeds), "r" ReInitGPU(0), "S" move sphere 6 by +1 in x and
+// ReInitSceneGPU (the keyboard handler's edit, displayfunc.cpp:300-420) --
+// and writes pixels (W*H u32), the device HDR colours (3*W*H f32), the seeds
+// the last AllocateBuffers drew, currentSample, the number of row bands and
+// currentSample after each step to argv[4].
 #include <stdio.h>
 #include <stdlib.h>
 #include <sys/time.h>
+#include <vector>
 #include "../../include/rt_hip.h"
 #include "../../oracle/oracle.h"
 
@@ -22,6 +28,8 @@ extern unsigned int sphereCount;
 void SetUpHIP();
 void UpdateRenderingGPU();
 void ReInitGPU(const int);
+void ReInitSceneGPU();
+int SmallptHipBands();
 void SmallptHipReadColors(float *out);
 const unsigned int *SmallptHipInitialSeeds();
 
@@ -49,7 +57,31 @@ int main(int argc, char **argv)
     if (rt_device_count() < 1) { fprintf(stderr, "no HIP device\n"); return 1; }
     srand(1);
     SetUpHIP();
-    for (int i = 0; i < passes; i++) UpdateRenderingGPU();
+    std::vector<int> after;
+    if (argc > 5) {
+        for (const char *p = argv[5]; *p;) {
+            if (*p == 'p') {
+                char *end;
+                const long n = strtol(p + 1, &end, 10);
+                for (long i = 0; i < n; i++) UpdateRenderingGPU();
+                p = end;
+            } else if (*p == 'R' || *p == 'r') {
+                ReInitGPU(*p == 'R');
+                p++;
+            } else if (*p == 'S') {
+                cs[6].p.x += 1.f;
+                ReInitSceneGPU();
+                p++;
+            } else {
+                fprintf(stderr, "bad script step '%c'\n", *p);
+                return 2;
+            }
+            after.push_back(currentSample);
+            if (*p == ',') p++;
+        }
+    } else {
+        for (int i = 0; i < passes; i++) UpdateRenderingGPU();
+    }
     float *col = (float *)malloc(sizeof(float) * 3 * width * height);
     SmallptHipReadColors(col);
     FILE *f = fopen(argv[4], "wb");
@@ -57,6 +89,9 @@ int main(int argc, char **argv)
     fwrite(col, 4, (size_t)3 * width * height, f);
     fwrite(SmallptHipInitialSeeds(), 4, (size_t)2 * width * height, f);
     fwrite(&currentSample, 4, 1, f);
+    const int bands = SmallptHipBands();
+    fwrite(&bands, 4, 1, f);
+    if (!after.empty()) fwrite(after.data(), 4, after.size(), f);
     fclose(f);
     fprintf(stderr, "%s", captionBuffer);
     return 0;

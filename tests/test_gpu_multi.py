@@ -1,0 +1,132 @@
+"""smallpt frames tiled over several GPUs behind the C-ABI (spt_render_multi,
+spt_multi_*; SURVEY.md §8(b) "spt_render(..., ngpus)", §8(e) row bands).
+
+A device may repeat in the device list, so the band / assemble code runs
+with N bands on a one-GPU box exactly as it runs over N GPUs; with distinct
+devices the gather is an RCCL group (RT_SPT_GATHER=rccl forces that path even
+for one band).  Every result must equal the single-GPU frame bit for bit,
+which the other GPU tests pin to the reference."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "known_answers.json")
+
+
+def _frame(rt, w, h, spp, devices=None, first=0, counters=True):
+    f = rt.SmallptFrame(w, h)
+    if first:
+        f.render(first, counters=False)
+    f.render(spp, counters=counters, devices=devices)
+    return f
+
+
+def _same(a, b):
+    assert (a.colors.view(np.uint32) == b.colors.view(np.uint32)).all()
+    assert (a.seeds == b.seeds).all() and (a.pixels == b.pixels).all()
+
+
+def test_render_multi_one_device_equals_single(rt):
+    a = _frame(rt, 320, 240, 4)
+    b = _frame(rt, 320, 240, 4, devices=[0])
+    _same(a, b)
+    assert a.counters == b.counters
+
+
+@pytest.mark.parametrize("nb,w,h", [(2, 320, 240), (3, 197, 241), (5, 64, 7), (7, 160, 120)])
+def test_render_multi_repeated_device_bands(rt, nb, w, h):
+    """nb bands on device 0 (ragged: h not a multiple of nb, bands of 1-2
+    rows), continuing a progressive frame (first_sample > 0: the
+    accumulator is uploaded per band too)."""
+    a = _frame(rt, w, h, 3, first=2)
+    b = _frame(rt, w, h, 3, devices=[0] * nb, first=2)
+    _same(a, b)
+    assert a.counters == b.counters
+
+
+def test_render_multi_direct_lighting(rt):
+    a = rt.SmallptFrame(160, 120, mode=rt.SPT_DIRECT_LIGHTING).render(3)
+    b = rt.SmallptFrame(160, 120, mode=rt.SPT_DIRECT_LIGHTING).render(3, devices=[0, 0, 0])
+    _same(a, b)
+
+
+@pytest.mark.parametrize("gather", ["peer", "rccl"])
+def test_multi_context_progressive_and_gather(rt, gather, monkeypatch):
+    """Device-resident progressive passes on a band context, then the gather:
+    every band's device then holds the whole frame (HDR + repacked RGBA8)."""
+    w, h = 256, 192
+    nb = 4 if gather == "peer" else 1          # RCCL needs distinct devices: one band here
+    monkeypatch.setenv("RT_SPT_GATHER", gather)
+    cam = rt.scenes.cornell_camera(w, h)
+    m = rt.SmallptMulti(w, h, [0] * nb)
+    assert m.rows[0] == 0 and m.rows[-1] == h and len(m.rows) == nb + 1
+    seeds = rt.scenes.seeds(w, h)
+    m.upload(seeds)
+    for k in range(3):                          # three UpdateRenderingGPU-style passes
+        m.render(cam, k, 1, counters=True)
+    m.gather()
+    m.sync()
+    ref = _frame(rt, w, h, 3)
+    for k in range(nb):
+        col, px = m.read_frame(k)
+        assert (col.view(np.uint32) == ref.colors.view(np.uint32)).all(), k
+        assert (px == ref.pixels).all(), k
+    col, sd, px = np.empty_like(ref.colors), np.empty_like(ref.seeds), np.empty_like(ref.pixels)
+    m.download(col, sd, px)
+    assert (col.view(np.uint32) == ref.colors.view(np.uint32)).all() and (sd == ref.seeds).all()
+    assert (px == ref.pixels).all()
+    assert m.counters() == ref.counters
+    # a second frame after the gather (the peer copies are ordered before the
+    # next render overwrites a band's rows)
+    m.render(cam, 3, 2)
+    m.gather()
+    m.sync()
+    ref.render(2)
+    for k in range(nb):
+        col, px = m.read_frame(k)
+        assert (col.view(np.uint32) == ref.colors.view(np.uint32)).all() and (px == ref.pixels).all(), k
+    m.close()
+
+
+def test_multi_scene_update(rt):
+    """spt_multi_set_scene (ReInitSceneGPU) re-uploads the edited scene to
+    every band."""
+    w, h = 160, 120
+    S, n = rt.scenes.cornell()
+    cam = rt.scenes.cornell_camera(w, h)
+    m = rt.SmallptMulti(w, h, [0, 0], S, n)
+    m.upload(rt.scenes.seeds(w, h))
+    m.render(cam, 0, 2)
+    S[6].p.x += 1.0
+    m.set_scene(S, n)
+    m.render(cam, 0, 2)
+    col, px = np.empty(3 * w * h, np.float32), np.empty(w * h, np.uint32)
+    m.download(col, None, px)
+    f = rt.SmallptFrame(w, h)
+    f.render(2)
+    f.spheres = S
+    f.current_sample = 0
+    f.render(2)
+    assert (col.view(np.uint32) == f.colors.view(np.uint32)).all() and (px == f.pixels).all()
+
+
+def test_render_multi_full_frame_golden(rt, oracle):
+    """BASELINE configs[3]'s frame (Cornell 1920x1080, 64 spp) in eight row
+    bands on one device (the N = 8 decomposition), against the reference-
+    core golden hashes."""
+    ka = json.load(open(GOLDEN))["smallpt"]["1920x1080_64spp"]
+    f = _frame(rt, 1920, 1080, 64, devices=[0] * 8, counters=False)
+    assert oracle.fnv1a64(f.colors) == ka["colors"]
+    assert oracle.fnv1a64(f.pixels) == ka["pixels"]
+    assert oracle.fnv1a64(f.seeds) == ka["seeds"]
+
+
+def test_multi_bad_arguments(rt):
+    S, n = rt.scenes.cornell()
+    with pytest.raises(rt.RTError):
+        rt.SmallptMulti(64, 4, [0] * 5, S, n)       # more bands than rows
+    with pytest.raises(rt.RTError):
+        rt.SmallptMulti(64, 64, [rt.device_count()], S, n)
