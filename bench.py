@@ -77,6 +77,9 @@ def cpu_baseline(args):
     workload: rows of the 1920x1080 Cornell frame at 64 spp, sized to about
     args.cpu_seconds of host time."""
     import oracle_lib as O
+    # OMP_NUM_THREADS is the host-CPU share of one GPU job on the MI355X pool
+    # (16 of the node's 256 CPUs, set by the pool for every job); all 256 are
+    # not ours to use.
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     S, n = O.cornell()
     cam = O.cornell_camera(W, H)
@@ -101,7 +104,8 @@ def cpu_baseline(args):
            "sample": "oracle/smallpt_oracle.c, rows [%d,%d) of the 1920x1080 Cornell frame at 64 spp "
                      "(%d samples, %.1f s, %d threads; %.3f Msamples/s)"
                      % (r0, r0 + rows2, c[3], dt, threads, c[3] / dt / 1e6),
-           "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
+           "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+           "cores_note": "OMP_NUM_THREADS: the pool's host-CPU share of a one-GPU job (16 of the node's CPUs)"}
     # The reference's own code (oracle/_ref: RadiancePathTracing & co. of
     # smallptgpu-v1.6 compiled from its sources) on one thread, as the
     # reference's CPU path runs; rays counted by the port on the same band
@@ -167,7 +171,8 @@ def whitted_line(args, dev):
     rays = counts[0] + counts[1]
     out = {"workload": "Whitted raytracer3.0.06 scene 1920x1080, 9 primary rays/px, rows [20,1010)",
            "ms_per_frame": round(ms, 4), "Mrays_per_s": round(rays / ms / 1e3, 2),
-           "rays_per_frame": rays, "ray_prim_tests": counts[2]}
+           "rays_per_frame": rays, "ray_prim_tests": counts[2],
+           "device_bytes": int(L.rt_cached_bytes())}
     if not args.no_cpu:
         import oracle_lib as O
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
@@ -178,6 +183,47 @@ def whitted_line(args, dev):
                                "cores": threads, "kind": "port", "ms_per_frame": round(dt * 1e3, 1),
                                "sample": "oracle/whitted_oracle.c, the full frame"}
     return out
+
+
+def configs0_line(args, dev):
+    """Side line: BASELINE configs[0], the Whitted scene at 640x480 on the CPU
+    path -- the reference's own timing loop (testapp.cpp:142-155: one
+    Engine_InitRender + Engine_Render per run) restated by the oracle, on one
+    thread as the reference runs and on the host share -- with the same frame
+    on the GPU beside it."""
+    import oracle_lib as O
+    w, h = 640, 480
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    _, c = O.whitted_render(w, h, nthreads=1)
+    dt1 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    O.whitted_render(w, h, nthreads=threads)
+    dtn = time.perf_counter() - t0
+    rays = c[0] + c[1]
+    prims, n = rtamd.scenes.whitted_scene()
+    d_prims = torch.frombuffer(bytearray(bytes(prims)), dtype=torch.uint8).to(dev)
+    frame = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    L = rtamd.lib()
+    run = lambda: rtamd.check(L.rtw_render_async(d_prims.data_ptr(), n, frame.data_ptr(), w, h, 20, h - 70,  # noqa: E731
+                                                 None, s.cuda_stream))
+    run()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(10):
+        run()
+    e1.record(s)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / 10
+    return {"workload": "configs[0]: Whitted raytracer3.0.06 scene 640x480, rows [20,410), CPU path",
+            "rays_per_frame": rays,
+            "cpu_1thread": {"ms_per_frame": round(dt1 * 1e3, 1), "Mrays_per_s": round(rays / dt1 / 1e6, 3),
+                            "cores": 1, "kind": "port", "sample": "oracle/whitted_oracle.c, the full frame"},
+            "cpu_threads": {"ms_per_frame": round(dtn * 1e3, 1), "Mrays_per_s": round(rays / dtn / 1e6, 3),
+                            "cores": threads, "kind": "port", "sample": "oracle/whitted_oracle.c, the full frame"},
+            "gpu": {"ms_per_frame": round(ms, 4), "Mrays_per_s": round(rays / ms / 1e3, 2)}}
 
 
 def c5_line(args, dev):
@@ -405,6 +451,8 @@ def main():
         if not args.no_whitted:
             out["whitted"] = whitted_line(args, dev)
             out["configs4"] = c5_line(args, dev)
+            if not args.no_cpu:
+                out["configs0"] = configs0_line(args, dev)
         out["cpu_baseline"] = None if args.no_cpu else cpu_baseline(args)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -22,8 +22,10 @@ void release_state(DeviceState *st)
     if (!st) return;
     (void)hipSetDevice(st->device);
     if (st->stream) (void)hipStreamSynchronize(st->stream);
+    if (st->wf_done) (void)hipEventSynchronize(st->wf_done);
     for (int i = 0; i < NSCRATCH; i++)
         if (st->buf[i]) (void)hipFree(st->buf[i]);
+    if (st->wf_done) (void)hipEventDestroy(st->wf_done);
     if (st->stream) (void)hipStreamDestroy(st->stream);
     delete st;
 }
@@ -74,6 +76,12 @@ int state(DeviceState **out)
         st->cus = prop.multiProcessorCount;
         e = hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking);
         if (e != hipSuccess) { delete st; return fail_hip(e, "hipStreamCreate"); }
+        e = hipEventCreateWithFlags(&st->wf_done, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            (void)hipStreamDestroy(st->stream);
+            delete st;
+            return fail_hip(e, "hipEventCreate");
+        }
         g_states[dev] = st;
     } else {
         hipError_t e = hipSetDevice(dev);

@@ -5,6 +5,7 @@
 #define RT_RUNTIME_H
 
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include <stddef.h>
 #include "../../include/rt_hip.h"
 
@@ -20,11 +21,19 @@ struct DeviceState {
     void *buf[NSCRATCH] = {};          // grow-only device buffers
     size_t cap[NSCRATCH] = {};
     size_t cached_bytes = 0;
-    // Whitted m_SX/m_SY tables for frame size (vt_w, vt_h) in scratch slot
-    // SLOT_VIEW (whitted.hip).
-    int vt_w = 0, vt_h = 0;
-    float vt_DX = 0.f, vt_DY = 0.f;
-    int vto_w = 0, vto_h = 0;          // openCLcode.cl-semantics tables (whitted.hip)
+    // Held by an entry point while it uses this state's buffers / stream
+    // (recursive: the blocking entry points call the asynchronous ones).
+    std::recursive_mutex mu;
+    // Whitted view tables (m_SX / m_SY, or openCLcode.cl's) for frame size
+    // (vt_w, vt_h) and semantics vt_ocl in scratch slot SLOT_VIEW, and the
+    // level-pass arena: both are reused by every frame on this device, on
+    // whatever stream it is issued.  wf_done is recorded after each frame's
+    // kernels; the next frame's stream waits on it (frames on different
+    // streams are serialised, never interleaved), and a buffer is regrown
+    // only after it has completed (whitted.hip).
+    int vt_w = 0, vt_h = 0, vt_ocl = -1;
+    hipEvent_t wf_done = nullptr;
+    bool wf_pending = false;
 };
 
 // Records msg (plus the HIP error string) for rt_last_error(); returns code.

@@ -359,34 +359,43 @@ __device__ __forceinline__ void load_scene(Scene &S, const Scene *__restrict__ g
 //   root_kernel    level 0 of every tree (coherent: one launch, lanes = pixels);
 //   level_kernel   level L = 1..5 from a compacted queue of child rays that
 //                  level L-1 appended (wave-aggregated atomics);
+//   tir_kernel     after level L: the refraction children of its TIR nodes
+//                  (see below), appended to level L+1;
 //   backacc_kernel levels 4..1: node colour += refraction child (Beer factor)
 //                  then += reflection child (:476-511), children final first;
 //   final_kernel   level 0 of the nine trees of a pixel + the sum / x28 pack.
 // Records hold what back-accumulation needs (colour, distance, primitive, TIR)
 // and the queue slots of the node's two children.
 //
+// Queue memory.  Levels 1..5 share ONE pool of records.  Each level's queue
+// is split into NSEG segments with their own counters (a producing wave
+// appends to segment wave_id mod NSEG, so thousands of waves finishing a step
+// together do not queue on one atomic address); a segment's items are laid
+// out in 64-slot pages, page c of segment s at level base + (c*NSEG + s)*64.
+// Level L+1 starts right after level L's last page (base_{L+1} = base_L +
+// NSEG*64*max_s pages_s, computed by level_kernel(L) once level L is final),
+// so the pool holds the levels' actual node counts (14.2 M at 1080p for 17.1 M
+// trees), not a per-level worst case.
+//
 // Exceptions go to fixup_kernel, which re-evaluates the whole tree in the
-// reference's sequential BFS order (per-lane records):
-//   * TIR: the reference still traces p's refraction child, with the
-//     refraction ray of the last node BEFORE p in BFS order that wrote one
-//     (:231-233, a stale variable) -- a cross-node dependency.  The wavefront
-//     does not trace that child and flags the tree;
-//   * a full child queue (capacity = number of trees per level).
-// The fixup counts only the nodes the wavefront did not trace, so counters
-// stay exactly the reference's.
+// reference's sequential BFS order (per-lane records): a tree with a node
+// that does not fit in the pool, or a TIR whose stale ray (below) is not in
+// the pool.  The fixup counts only the nodes the wavefront did not trace, so
+// counters stay exactly the reference's.
 constexpr int LEVELS = 6;
 constexpr int INFO_TIR = 0x100;       // refr > 0 but no refraction ray (TIR)
 constexpr int INFO_REFR_OK = 0x200;   // the node wrote a refraction ray
-// Each level's queue is split into NSEG segments with their own counters: a
-// producing wave appends to segment (wave id mod NSEG), so thousands of
-// waves finishing a step together do not queue on one atomic address.
+constexpr int NODE_SHIFT = 16;        // linfo bits 16..21: the node's index (0..62)
 constexpr int NSEG = 64;
-// count[] layout (zeroed per frame).  Every counter has its own 128-B line
+constexpr int PAGE = 64;              // slots per page (one segment's)
+constexpr int PAGE_ROW = NSEG * PAGE; // one page of every segment
+// count[] layout (zeroed per slab).  Every counter has its own 128-B line
 // (same-line atomics serialise in the L2's atomic unit).
 constexpr int CSTRIDE = 32;
-constexpr int C_FIX = 0;                      // fixup list length
+constexpr int C_FIX = 0;                      // trees flagged for fixup
 constexpr int C_TIR = 1;                      // + L: TIR list length of level L (0..4)
-constexpr int C_SEG = C_TIR + LEVELS;         // + L * NSEG + s: length of segment s of level L (1..5)
+constexpr int C_BASE = C_TIR + LEVELS;        // + L: pool base of level L (2..5; level 1 at 0)
+constexpr int C_SEG = C_BASE + LEVELS;        // + L * NSEG + s: length of segment s of level L (1..5)
 constexpr int C_TOTAL = C_SEG + LEVELS * NSEG;
 #define CNT(A, i) ((A).count[(i) * CSTRIDE])
 
@@ -396,32 +405,62 @@ struct WfArgs {
     int *rinfo;               // [ntrees] hit primitive | INFO_*
     float4 *psum;             // [npix] sum (xyz) of the colours of the pixel's leading childless trees,
                               //   in sub-sample order, and (w, int bits) the first sub-sample not in it
-    int2 *rchild;             // [ntrees] queue slots (level 1) of refl / refr child, -1 if none
-    int *fixflag;             // [ntrees] 0, or -1 once queued for fixup
-    int *fixlist;             // [ntrees] trees to fix
-    float4 *ia[LEVELS];       // [cap] queued ray: o.xyz, d.x
-    float4 *ib[LEVELS];       // [cap] d.y, d.z, rindex, tree (int bits)
-    int *lnode[LEVELS];       // [cap] the node's index in the reference's 63-slot array
-    float4 *lcol[LEVELS];     // [cap] node colour.xyz, dist
-    int *linfo[LEVELS];       // [cap] hit primitive | INFO_*
-    int2 *lchild[LEVELS];     // [cap] child slots in level L+1
-    int4 *tir[LEVELS];        // [tcap] TIR nodes of level L: slot, tree, node, rindex (bits)
+    int2 *rchild;             // [ntrees] pool slots (level 1) of refl / refr child, -1 if none
+    unsigned *fixbits;        // [ntrees/32 + 1] tree flagged for fixup
+    int *fixlist;             // [fixcap] flagged trees (fixup scans fixbits when more)
+    // The record pool (levels 1..5), indexed by pool slot.
+    float4 *ia;               // queued ray: o.xyz, d.x
+    float4 *ib;               // d.y, d.z, rindex, tree (int bits)
+    float4 *lcol;             // node colour.xyz, dist
+    int *linfo;               // node << NODE_SHIFT (queued), then | hit primitive | INFO_* (traced)
+    int2 *lchild;             // pool slots of the node's children
+    int4 *tir[LEVELS];        // [tcap] TIR nodes of level L (0..4): slot, tree, node, rindex (bits)
     int *count;               // [C_TOTAL * CSTRIDE]
-    int cap, segcap, tcap, ntrees, npix, w, row_begin;   // cap = NSEG * segcap
+    int pool, fixcap, tcap, ntrees, npix, w;
+    int row_begin, row_stride;   // the slab's rows: see slab_row
     int side, nsub;           // sub-sample grid: 3 x 3 (CPU path) or 2 x 2 (openCLcode.cl)
     bool ocl;                 // openCLcode.cl semantics (light colour, refl-first folding, x64)
 };
 
+// Row y of the slab's local row r: slabs interleave in groups of 16 rows (a
+// root block's height), group g of the slab at frame group g*row_stride + k
+// (row_begin = first row + 16k).
+__device__ __forceinline__ int slab_row(const WfArgs &A, int r)
+{
+    return A.row_begin + ((r >> 4) * A.row_stride << 4) + (r & 15);
+}
+
+// Pool slot of item j of segment s of the level based at `base`, and the
+// per-segment item limit of that level (the pages left in the pool).
+__device__ __forceinline__ int seg_slot(int base, int s, int j)
+{
+    return base + ((j >> 6) * NSEG + s) * PAGE + (j & (PAGE - 1));
+}
+__device__ __forceinline__ int seg_limit(const WfArgs &A, int base)
+{
+    return (A.pool - base) / PAGE_ROW * PAGE;
+}
+__device__ __forceinline__ int level_base(const WfArgs &A, int L)
+{
+    return L <= 1 ? 0 : CNT(A, C_BASE + L);
+}
+
 __device__ void flag_tree(const WfArgs &A, int tree)
 {
-    if (atomicCAS(&A.fixflag[tree], 0, -1) == 0) {
+    const unsigned bit = 1u << (tree & 31);
+    if (!(atomicOr(&A.fixbits[tree >> 5], bit) & bit)) {
         const int s = atomicAdd(&CNT(A, C_FIX), 1);
-        A.fixlist[s] = tree;
+        if (s < A.fixcap) A.fixlist[s] = tree;
     }
 }
 
+__device__ __forceinline__ bool flagged(const WfArgs &A, int tree)
+{
+    return (A.fixbits[tree >> 5] >> (tree & 31)) & 1u;
+}
+
 // Wave-aggregated queue allocation: every active lane asks for `want` (0..2)
-// slots; one atomic per wave.  Returns the lane's first slot.
+// items; one atomic per wave.  Returns the lane's first item index.
 __device__ __forceinline__ int wave_alloc(int *counter, int want)
 {
     const unsigned long long m1 = __builtin_amdgcn_ballot_w64((want & 1) != 0);
@@ -440,36 +479,37 @@ __device__ __forceinline__ int wave_alloc(int *counter, int want)
 __device__ __forceinline__ void put_item(const WfArgs &A, int L, int slot, const ray3 &r, float rin, int tree,
                                          int node)
 {
-    A.ia[L][slot] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-    A.ib[L][slot] = make_float4(r.d.y, r.d.z, rin, __int_as_float(tree));
-    A.lnode[L][slot] = node;
+    A.ia[slot] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+    A.ib[slot] = make_float4(r.d.y, r.d.z, rin, __int_as_float(tree));
+    if (L < LEVELS - 1) A.linfo[slot] = node << NODE_SHIFT;   // level 5 needs no node index
 }
 
-// Queues the children of node `node` (level L < 5, record `slot`) into level
-// L+1 and returns their slots (-1: not queued).  A TIR node's refraction child
-// is queued later by tir_kernel, once every node before it in BFS order has
-// been traced.  All lanes of the wave call it.
-__device__ __forceinline__ int2 queue_children(const WfArgs &A, int L, int wave_id, bool active, int slot_self,
-                                               int tree, int node, const Hit &hh, bool tir)
+// Queues the children of node `node` (level L < 5, record `slot_self`) into
+// level L+1 (pool base `nbase`) and returns their slots (-1: not queued).  A
+// TIR node's refraction child is queued later by tir_kernel, once every node
+// before it in BFS order has been traced.  All lanes of the wave call it.
+__device__ __forceinline__ int2 queue_children(const WfArgs &A, int L, int nbase, int wave_id, bool active,
+                                               int slot_self, int tree, int node, const Hit &hh, bool tir)
 {
     const bool cl = active && hh.refl > 0, cr = active && hh.refr > 0;
     const bool qr = cr && !tir;
     const int seg = wave_id & (NSEG - 1);
-    int slot = wave_alloc(&CNT(A, C_SEG + (L + 1) * NSEG + seg), (int)cl + (int)qr);
+    const int lim = seg_limit(A, nbase);
+    int j = wave_alloc(&CNT(A, C_SEG + (L + 1) * NSEG + seg), (int)cl + (int)qr);
     int2 ch = make_int2(-1, -1);
     if (cl) {
-        if (slot < A.segcap) {
-            put_item(A, L + 1, seg * A.segcap + slot, hh.refl_ray, hh.rindex_out, tree, 2 * node + 1);
-            ch.x = seg * A.segcap + slot;
+        if (j < lim) {
+            ch.x = seg_slot(nbase, seg, j);
+            put_item(A, L + 1, ch.x, hh.refl_ray, hh.rindex_out, tree, 2 * node + 1);
         } else {
             flag_tree(A, tree);
         }
-        slot++;
+        j++;
     }
     if (qr) {
-        if (slot < A.segcap) {
-            put_item(A, L + 1, seg * A.segcap + slot, hh.refr_ray, hh.rindex_out, tree, 2 * node + 2);
-            ch.y = seg * A.segcap + slot;
+        if (j < lim) {
+            ch.y = seg_slot(nbase, seg, j);
+            put_item(A, L + 1, ch.y, hh.refr_ray, hh.rindex_out, tree, 2 * node + 2);
         } else {
             flag_tree(A, tree);
         }
@@ -488,15 +528,16 @@ __device__ __forceinline__ int node_info(const Hit &hh, bool tir)
 }
 
 // Consumer view of level L's segmented queue: lane s holds segment s's length
-// and the inclusive prefix of its 64-item chunk counts.  Whole waves only.
-struct SegView { int incl, n; };
+// and the inclusive prefix of its 64-item page counts.  Whole waves only.
+struct SegView { int incl, n, base; };
 
 __device__ __forceinline__ SegView seg_view(const WfArgs &A, int L)
 {
     const int lane = __lane_id();
     SegView v;
-    v.n = min(CNT(A, C_SEG + L * NSEG + lane), A.segcap);
-    int x = (v.n + 63) >> 6;
+    v.base = level_base(A, L);
+    v.n = min(CNT(A, C_SEG + L * NSEG + lane), seg_limit(A, v.base));
+    int x = (v.n + PAGE - 1) / PAGE;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const int y = __shfl_up(x, off, 64);
@@ -506,16 +547,25 @@ __device__ __forceinline__ SegView seg_view(const WfArgs &A, int L)
     return v;
 }
 
-// Chunk k (wave-uniform) of the queue: first slot and number of valid items;
-// false once k is past the last chunk.
-__device__ __forceinline__ bool seg_chunk(const WfArgs &A, const SegView &v, int k, int &base, int &nvalid)
+// The pool base after level L: past the last page of its fullest segment.
+__device__ __forceinline__ int next_base(const SegView &v)
+{
+    int p = (v.n + PAGE - 1) / PAGE;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) p = max(p, __shfl_xor(p, off, 64));
+    return v.base + p * PAGE_ROW;
+}
+
+// Page k (wave-uniform) of the queue: first slot and number of valid items;
+// false once k is past the last page.
+__device__ __forceinline__ bool seg_chunk(const SegView &v, int k, int &base, int &nvalid)
 {
     if (k >= __shfl(v.incl, 63, 64)) return false;
     const int s = __popcll(__builtin_amdgcn_ballot_w64(v.incl <= k));
     const int incl = __shfl(v.incl, s, 64), n = __shfl(v.n, s, 64);
-    const int c = k - (incl - ((n + 63) >> 6));
-    base = s * A.segcap + c * 64;
-    nvalid = min(64, n - c * 64);
+    const int c = k - (incl - ((n + PAGE - 1) / PAGE));
+    base = seg_slot(v.base, s, c * PAGE);
+    nvalid = min(PAGE, n - c * PAGE);
     return true;
 }
 
@@ -532,9 +582,10 @@ root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float
     load_scene(S, A.scene);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int y = A.row_begin + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int r = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);   // the slab's row r
+    const int y = slab_row(A, r);
     const bool active = x < A.w && y < row_end;
-    const int pix = (y - A.row_begin) * A.w + x;
+    const int pix = r * A.w + x;
     const float SX = active ? sx_tab[x] : 0.f, SY = active ? sy_tab[y] : 0.f;
     Counts cnt = {0, 0, 0, 0};
     // A tree without children (a plane, a light, a miss) is final at its
@@ -554,7 +605,7 @@ root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float
         }
         const int tree = sub * A.npix + pix;
         const int wave_id = ((blockIdx.y * gridDim.x + blockIdx.x) << 2) + wave;
-        const int2 ch = queue_children(A, 0, wave_id, active, tree, tree, 0, hh, tir);
+        const int2 ch = queue_children(A, 0, 0, wave_id, active, tree, tree, 0, hh, tir);
         if (active) {
             if (kfirst == A.nsub && !(hh.refl > 0 || hh.refr > 0)) {
                 tr += hh.acc.x; tg += hh.acc.y; tb += hh.acc.z;
@@ -573,7 +624,7 @@ root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float
     }
 }
 
-// Level L = 1..5: a grid of resident blocks; wave w takes 64-ray chunks
+// Level L = 1..5: a grid of resident blocks; wave w takes 64-ray pages
 // w, w + #waves, ... of the level's queue.
 template <bool COUNT>
 __global__ void __launch_bounds__(256, RT_WH_MINWAVES)
@@ -582,19 +633,21 @@ level_kernel(WfArgs A, int L, unsigned long long *__restrict__ counters)
     __shared__ Scene S;
     load_scene(S, A.scene);
     const SegView v = seg_view(A, L);
+    const int nbase = next_base(v);                 // level L+1's pool base
+    if (L < LEVELS - 1 && blockIdx.x == 0 && threadIdx.x == 0) CNT(A, C_BASE + L + 1) = nbase;
     const int lane = __lane_id();
     const int wave_id = (blockIdx.x << 2) + (threadIdx.x >> 6);
     Counts cnt = {0, 0, 0, 0};
     int base, nvalid;
-    for (int k = wave_id; seg_chunk(A, v, k, base, nvalid); k += gridDim.x << 2) {
+    for (int k = wave_id; seg_chunk(v, k, base, nvalid); k += gridDim.x << 2) {
         const int q = base + lane;
         const bool active = lane < nvalid;
         Hit hh;
         bool tir = false;
         int tree = 0, node = 0;
         if (active) {
-            const float4 a = A.ia[L][q], b = A.ib[L][q];
-            node = A.lnode[L][q];
+            const float4 a = A.ia[q], b = A.ib[q];
+            node = L < LEVELS - 1 ? A.linfo[q] >> NODE_SHIFT : 0;
             ray3 r;
             r.o = mk(a.x, a.y, a.z);
             r.d = mk(a.w, b.x, b.y);
@@ -602,12 +655,12 @@ level_kernel(WfArgs A, int L, unsigned long long *__restrict__ counters)
             hh = trace<COUNT>(S, r, b.z, cnt, A.ocl);
             tir = hh.refr > 0 && !hh.refr_ray_ok;
             if (tir && L < 5) cnt.tir++;                // node index < 31 (:398)
-            A.lcol[L][q] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
-            A.linfo[L][q] = node_info(hh, tir);
+            A.lcol[q] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
+            if (L < LEVELS - 1) A.linfo[q] = node_info(hh, tir);   // level 5's info has no reader
         }
-        if (L < 5) {
-            const int2 ch = queue_children(A, L, wave_id, active, q, tree, node, hh, tir);
-            if (active) A.lchild[L][q] = ch;
+        if (L < LEVELS - 1) {
+            const int2 ch = queue_children(A, L, nbase, wave_id, active, q, tree, node, hh, tir);
+            if (active) A.lchild[q] = ch;
         }
     }
     if (COUNT) {
@@ -626,7 +679,7 @@ __device__ bool find_node(const WfArgs &A, int tree, int j, int &lvl, int &slot)
     slot = tree;
     lvl = 0;
     for (int k = depth - 1; k >= 0; k--) {
-        const int2 ch = lvl == 0 ? A.rchild[slot] : A.lchild[lvl][slot];
+        const int2 ch = lvl == 0 ? A.rchild[slot] : A.lchild[slot];
         slot = ((h >> k) & 1u) ? ch.y : ch.x;
         lvl++;
         if (slot < 0) return false;
@@ -644,6 +697,8 @@ tir_kernel(WfArgs A, int L, const float *__restrict__ sx_tab, const float *__res
            float DY)
 {
     const int nt = min(CNT(A, C_TIR + L), A.tcap);
+    const int nbase = level_base(A, L + 1);
+    const int lim = seg_limit(A, nbase);
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
         const int4 e = A.tir[L][t];
         const int slot_self = e.x, tree = e.y, node = e.z;
@@ -653,11 +708,11 @@ tir_kernel(WfArgs A, int L, const float *__restrict__ sx_tab, const float *__res
         for (int j = node - 1; j >= 0 && !found && !broken; j--) {
             int lv, sl;
             if (!find_node(A, tree, j, lv, sl)) continue;
-            const int info = lv == 0 ? A.rinfo[sl] : A.linfo[lv][sl];
+            const int info = lv == 0 ? A.rinfo[sl] : A.linfo[sl];
             if (!(info & INFO_REFR_OK)) continue;
-            const int c = (lv == 0 ? A.rchild[sl] : A.lchild[lv][sl]).y;   // its own refraction child
-            if (c < 0) { broken = true; break; }                          // not queued (overflow)
-            const float4 a = A.ia[lv + 1][c], b = A.ib[lv + 1][c];
+            const int c = (lv == 0 ? A.rchild[sl] : A.lchild[sl]).y;   // its own refraction child
+            if (c < 0) { broken = true; break; }                       // not queued (overflow)
+            const float4 a = A.ia[c], b = A.ib[c];
             r.o = mk(a.x, a.y, a.z);
             r.d = mk(a.w, b.x, b.y);
             found = true;
@@ -665,16 +720,16 @@ tir_kernel(WfArgs A, int L, const float *__restrict__ sx_tab, const float *__res
         if (broken) { flag_tree(A, tree); continue; }
         if (!found) {
             const int sub = tree / A.npix, pix = tree % A.npix;
-            const int x = pix % A.w, y = A.row_begin + pix / A.w;
+            const int x = pix % A.w, y = slab_row(A, pix / A.w);
             r = primary(sub, sx_tab[x], sy_tab[y], DX, DY, A.side);
         }
         const int seg = tree & (NSEG - 1);
         const int k = atomicAdd(&CNT(A, C_SEG + (L + 1) * NSEG + seg), 1);
-        if (k >= A.segcap) { flag_tree(A, tree); continue; }
-        const int q = seg * A.segcap + k;
+        if (k >= lim) { flag_tree(A, tree); continue; }
+        const int q = seg_slot(nbase, seg, k);
         put_item(A, L + 1, q, r, rin, tree, 2 * node + 2);
         if (L == 0) A.rchild[slot_self].y = q;
-        else A.lchild[L][slot_self].y = q;
+        else A.lchild[slot_self].y = q;
     }
 }
 
@@ -722,12 +777,12 @@ backacc_kernel(WfArgs A, int L)
     const SegView v = seg_view(A, L);
     const int lane = __lane_id();
     int base, nvalid;
-    for (int k = (blockIdx.x << 2) + (threadIdx.x >> 6); seg_chunk(A, v, k, base, nvalid); k += gridDim.x << 2) {
+    for (int k = (blockIdx.x << 2) + (threadIdx.x >> 6); seg_chunk(v, k, base, nvalid); k += gridDim.x << 2) {
         const int q = base + lane;
         if (lane >= nvalid) continue;
-        const int2 ch = A.lchild[L][q];
+        const int2 ch = A.lchild[q];
         if (ch.x < 0 && ch.y < 0) continue;
-        A.lcol[L][q] = accumulate(S, A.lcol[L][q], A.linfo[L][q], ch, A.lcol[L + 1], A.ocl);
+        A.lcol[q] = accumulate(S, A.lcol[q], A.linfo[q], ch, A.lcol, A.ocl);
     }
 }
 
@@ -740,17 +795,18 @@ final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
     load_scene(S, A.scene);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int y = A.row_begin + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int r = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int y = slab_row(A, r);
     if (x >= A.w || y >= row_end) return;
-    const int pix = (y - A.row_begin) * A.w + x;
+    const int pix = r * A.w + x;
     const float4 ps = A.psum[pix];                          // the leading childless trees, summed by root_kernel
     float tr = ps.x, tg = ps.y, tb = ps.z;
     for (int sub = __float_as_int(ps.w); sub < A.nsub; sub++) {
         const int tree = sub * A.npix + pix;
         float4 c0 = A.rcol[tree];
-        if (A.fixflag[tree] == 0) {
+        if (!flagged(A, tree)) {
             const int2 ch = A.rchild[tree];
-            if (ch.x >= 0 || ch.y >= 0) c0 = accumulate(S, c0, A.rinfo[tree], ch, A.lcol[1], A.ocl);
+            if (ch.x >= 0 || ch.y >= 0) c0 = accumulate(S, c0, A.rinfo[tree], ch, A.lcol, A.ocl);
         }
         tr += c0.x; tg += c0.y; tb += c0.z;
     }
@@ -788,11 +844,17 @@ fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict
     __shared__ Scene S;
     load_scene(S, A.scene);
     const int nfix = CNT(A, C_FIX);
+    const bool scan = nfix > A.fixcap;                  // the list overflowed: walk the bitmask
+    const int nitems = scan ? (A.ntrees + 31) >> 5 : nfix;
     Counts cnt = {0, 0, 0, 0};
-    for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < nfix; f += gridDim.x * blockDim.x) {
-        const int tree = A.fixlist[f];
+    for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < nitems; f += gridDim.x * blockDim.x) {
+      unsigned bits = scan ? A.fixbits[f] : 1u;
+      while (bits) {
+        const int bit = __builtin_ctz(bits);
+        bits &= bits - 1u;
+        const int tree = scan ? (f << 5) + bit : A.fixlist[f];
         const int sub = tree / A.npix, pix = tree % A.npix;
-        const int x = pix % A.w, y = A.row_begin + pix / A.w;
+        const int x = pix % A.w, y = slab_row(A, pix / A.w);
         NodeStore ns;
         unsigned long long todo = 1, traced = 0;
         const ray3 root = primary(sub, sx_tab[x], sy_tab[y], DX, DY, A.side);
@@ -814,7 +876,7 @@ fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict
                 rin = ns.rin[p];
                 if (ns.wf[p] >= 0) {
                     const int lp = level_of(p);
-                    const int2 ch = lp == 0 ? A.rchild[ns.wf[p]] : A.lchild[lp][ns.wf[p]];
+                    const int2 ch = lp == 0 ? A.rchild[ns.wf[p]] : A.lchild[ns.wf[p]];
                     wf = (i & 1) ? ch.x : ch.y;
                 }
             }
@@ -873,6 +935,7 @@ fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict
             ns.col[p] = pc;
         }
         A.rcol[tree] = ns.col[0];
+      }
     }
     if (COUNT) {
         const unsigned long long c[4] = {cnt.traced, cnt.shadow, cnt.tests, cnt.tir};
@@ -890,84 +953,108 @@ fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict
 
 namespace {
 
-constexpr int SLOT_WF = 6;      // rtrt scratch slot of the wavefront arena
+constexpr int SLOT_WF = 6;      // rtrt scratch slot of the level-pass arena
 
-// m_SX / m_SY tables (Engine_InitRender raytracer.cpp:278-294, then the
-// sequential m_SX += m_DX (:524) and m_SY += m_DY (:526)) -- host float adds,
-// uploaded once per frame size into the device state's SLOT_VIEW buffer.
-constexpr int SLOT_VIEW_OCL = 5;   // SX = WX1 + x*DX, SY = WY1 + y*DY (openCLcode.cl:22-23)
+// Trees per slab of the level pass.  A frame with more trees is rendered as
+// several slabs, one after the other on the stream, so the arena is sized
+// for one slab whatever the frame size (1080p: one slab; 4K: four).  Slabs
+// interleave in groups of 16 rows (slab_row), so every slab holds the
+// frame's mix of sphere / plane / background rows and so its queue fill.
+constexpr long long SLAB_TREES = 18000000;
+// Record pool (levels 1..5 together) as a fraction of the slab's trees.  The
+// reference scene needs 0.83 (14.2 M nodes for 17.1 M trees at 1080p); a
+// tree whose node does not fit is finished by fixup_kernel, exactly, so a
+// denser scene is slower, never wrong.
+constexpr double POOL_FRAC = 0.9;
 
-int view_tables_ocl(rtrt::DeviceState &st, int w, int h, const float **d_sx, const float **d_sy)
+// m_SX / m_SY (Engine_InitRender raytracer.cpp:278-294, then the sequential
+// m_SX += m_DX (:524) per pixel and m_SY += m_DY (:526) per row): lane 0
+// runs the x recurrence, lane 1 the y one, with the reference's float adds.
+// openCLcode.cl:22-23 semantics: SX = WX1 + x*DX, SY = WY1 + y*DY.
+__global__ void __launch_bounds__(64) view_kernel(float *__restrict__ tab, int w, int h, float DX, float DY, int ocl)
 {
-    void *d = nullptr;
-    int rc = rtrt::scratch(st, SLOT_VIEW_OCL, sizeof(float) * ((size_t)w + h), &d);
-    if (rc) return rc;
-    if (st.vto_w != w || st.vto_h != h) {
-        const float WX1 = -3.0f, WX2 = 3.0f, WY1 = 2.25f, WY2 = -2.25f;
-        const float DX = (WX2 - WX1) / w;
-        const float DY = (WY2 - WY1) / h;
-        float *tab = new float[(size_t)w + h];
-        for (int x = 0; x < w; x++) tab[x] = WX1 + x * DX;
-        for (int y = 0; y < h; y++) tab[w + y] = WY1 + y * DY;
-        hipError_t e = hipMemcpy(d, tab, sizeof(float) * ((size_t)w + h), hipMemcpyHostToDevice);
-        delete[] tab;
-        if (e != hipSuccess) return rtrt::fail_hip(e, "whitted view tables");
-        st.vto_w = w; st.vto_h = h;
+    const float WX1 = -3.0f, WY1 = 2.25f;
+    if (ocl) {
+        for (int i = threadIdx.x; i < w + h; i += 64)
+            tab[i] = i < w ? WX1 + i * DX : WY1 + (i - w) * DY;
+        return;
     }
-    *d_sx = (const float *)d;
-    *d_sy = (const float *)d + w;
-    return RT_OK;
-}
-
-int view_tables(rtrt::DeviceState &st, int w, int h, const float **d_sx, const float **d_sy)
-{
-    void *d = nullptr;
-    int rc = rtrt::scratch(st, rtrt::SLOT_VIEW, sizeof(float) * ((size_t)w + h), &d);
-    if (rc) return rc;
-    if (st.vt_w != w || st.vt_h != h) {
-        const float WX1 = -3, WX2 = 3, WY1 = 2.25f, WY2 = -2.25f;
-        const float DX = (WX2 - WX1) / w;
-        const float DY = (WY2 - WY1) / h;
-        float *tab = new float[(size_t)w + h];
+    if (threadIdx.x == 0) {
         float sx = WX1;
         for (int x = 0; x < w; x++) { tab[x] = sx; sx += DX; }
+    } else if (threadIdx.x == 1) {
         float sy = WY1;
         sy += 20 * DY;
-        for (int y = 0; y < h; y++) tab[w + y] = 0.f;
+        for (int y = 0; y < h && y < 20; y++) tab[w + y] = 0.f;
         for (int y = 20; y < h; y++) { tab[w + y] = sy; sy += DY; }
-        hipError_t e = hipMemcpy(d, tab, sizeof(float) * ((size_t)w + h), hipMemcpyHostToDevice);
-        delete[] tab;
-        if (e != hipSuccess) return rtrt::fail_hip(e, "whitted view tables");
-        st.vt_w = w; st.vt_h = h; st.vt_DX = DX; st.vt_DY = DY;
+    }
+}
+
+// Host wait for the previous frame (its arena, tables and staging slots).
+int wait_frame(rtrt::DeviceState &st)
+{
+    hipError_t e = hipEventSynchronize(st.wf_done);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtw frame wait");
+    st.wf_pending = false;
+    return RT_OK;
+}
+
+// Device slot of at least `bytes` that the previous frame may still read:
+// regrowing frees it, so wait for that frame first.
+int frame_scratch(rtrt::DeviceState &st, int slot, size_t bytes, void **out)
+{
+    if (st.cap[slot] < bytes && st.wf_pending) {
+        int rc = wait_frame(st);
+        if (rc) return rc;
+    }
+    return rtrt::scratch(st, slot, bytes, out);
+}
+
+// View tables for (w, h, ocl) in slot SLOT_VIEW, (re)computed on `s` only
+// when the frame size or semantics change (ordered after earlier frames by
+// the caller's wait on wf_done).
+int view_tables(rtrt::DeviceState &st, hipStream_t s, int w, int h, bool ocl, float DX, float DY,
+                const float **d_sx, const float **d_sy)
+{
+    void *d = nullptr;
+    int rc = frame_scratch(st, rtrt::SLOT_VIEW, sizeof(float) * ((size_t)w + h), &d);
+    if (rc) return rc;
+    if (st.vt_w != w || st.vt_h != h || st.vt_ocl != (int)ocl) {
+        hipLaunchKernelGGL(view_kernel, dim3(1), dim3(64), 0, s, (float *)d, w, h, DX, DY, (int)ocl);
+        if ((rc = rtrt::check_launch("rtw view_kernel"))) return rc;
+        st.vt_w = w; st.vt_h = h; st.vt_ocl = (int)ocl;
     }
     *d_sx = (const float *)d;
     *d_sy = (const float *)d + w;
     return RT_OK;
 }
 
-// Device arena of the wavefront pass (scratch slot SLOT_WF, grow-only):
-// per tree a root record, per level 1..5 a queue of capacity = #trees.
+// Device arena of the level pass (scratch slot SLOT_WF, grow-only) for a slab
+// of `rows` rows: per tree a root record and a fixup bit; the record pool of
+// levels 1..5; per level 0..4 a TIR list.
 int wavefront_arena(rtrt::DeviceState &st, int w, int rows, int nsub, rt::whitted::WfArgs *A)
 {
     using namespace rt::whitted;
     const size_t T = (size_t)w * rows * nsub;
     if (T > (size_t)0x7fffffff / 2) return rtrt::fail(RT_ERR_INVALID, "rtw: frame too large");
-    // Queue capacity per level: one slot per tree.  RT_WHITTED_QUEUE_CAP
-    // lowers it (test hook: exercises the overflow -> fixup path).
-    size_t C = T;
+    // RT_WHITTED_QUEUE_CAP lowers the pool (test hook: exercises the
+    // overflow -> fixup path).
+    size_t P = (size_t)(T * POOL_FRAC);
     if (const char *e = getenv("RT_WHITTED_QUEUE_CAP")) {
         const long long v = atoll(e);
-        if (v > 0 && (size_t)v < C) C = (size_t)v;
+        if (v > 0 && (size_t)v < P) P = (size_t)v;
     }
-    const size_t SC = (C + NSEG - 1) / NSEG;           // per-segment capacity
-    C = SC * NSEG;
-    const size_t TC = std::max<size_t>(C / 8, 1024);    // TIR list per level
+    P = std::max<size_t>((P + PAGE_ROW - 1) / PAGE_ROW, 1) * PAGE_ROW;
+    const size_t TC = std::max<size_t>(P / 64, 1024);   // TIR list per level
+    const size_t FC = std::max<size_t>(T / 16, 1024);   // fixup list
+    const size_t FB = (T + 31) / 32 * 4;                // fixup bits
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t root_b = al(T * 16) + al(T * 4) + al((size_t)w * rows * 16) + al(T * 8) + al(T * 4) + al(T * 4);
-    const size_t lvl_b = al(C * 16) * 3 + al(C * 4) * 2 + al(C * 8) + al(TC * 16);
-    const size_t bytes = al(sizeof(Scene)) + root_b + LEVELS * lvl_b + al(sizeof(int) * C_TOTAL * CSTRIDE);
+    const size_t root_b = al(T * 16) + al(T * 4) + al((size_t)w * rows * 16) + al(T * 8) + al(FB) + al(FC * 4);
+    const size_t pool_b = al(P * 16) * 3 + al(P * 4) + al(P * 8);
+    const size_t bytes = al(sizeof(Scene)) + root_b + pool_b + (LEVELS - 1) * al(TC * 16) +
+                         al(sizeof(int) * C_TOTAL * CSTRIDE);
     void *base = nullptr;
-    int rc = rtrt::scratch(st, SLOT_WF, bytes, &base);
+    int rc = frame_scratch(st, SLOT_WF, bytes, &base);
     if (rc) return rc;
     char *p = (char *)base;
     auto take = [&](size_t b) { char *q = p; p += al(b); return q; };
@@ -976,20 +1063,17 @@ int wavefront_arena(rtrt::DeviceState &st, int w, int rows, int nsub, rt::whitte
     A->rinfo = (int *)take(T * 4);
     A->psum = (float4 *)take((size_t)w * rows * 16);
     A->rchild = (int2 *)take(T * 8);
-    A->fixflag = (int *)take(T * 4);
-    A->fixlist = (int *)take(T * 4);
-    for (int L = 0; L < LEVELS; L++) {            // level 0 uses only its TIR list
-        A->ia[L] = (float4 *)take(C * 16);
-        A->ib[L] = (float4 *)take(C * 16);
-        A->lcol[L] = (float4 *)take(C * 16);
-        A->lnode[L] = (int *)take(C * 4);
-        A->linfo[L] = (int *)take(C * 4);
-        A->lchild[L] = (int2 *)take(C * 8);
-        A->tir[L] = (int4 *)take(TC * 16);
-    }
+    A->fixbits = (unsigned *)take(FB);
+    A->fixlist = (int *)take(FC * 4);
+    A->ia = (float4 *)take(P * 16);
+    A->ib = (float4 *)take(P * 16);
+    A->lcol = (float4 *)take(P * 16);
+    A->linfo = (int *)take(P * 4);
+    A->lchild = (int2 *)take(P * 8);
+    for (int L = 0; L < LEVELS; L++) A->tir[L] = L < LEVELS - 1 ? (int4 *)take(TC * 16) : nullptr;
     A->count = (int *)take(sizeof(int) * C_TOTAL * CSTRIDE);
-    A->cap = (int)C;
-    A->segcap = (int)SC;
+    A->pool = (int)P;
+    A->fixcap = (int)FC;
     A->tcap = (int)TC;
     A->ntrees = (int)T;
     A->npix = w * rows;
@@ -1009,15 +1093,13 @@ int resident_blocks(K kernel)
 }
 
 template <bool COUNT>
-int launch_wavefront(const rt_primitive *d_prims, int nprims, const rt::whitted::WfArgs &A, int w, int rows,
-                     int row_end, const float *d_sx, const float *d_sy, float DX, float DY,
-                     unsigned long long *cnt, hipStream_t s, uint32_t *d_xrgb)
+int launch_wavefront(const rt::whitted::WfArgs &A, int w, int rows, int row_end, const float *d_sx,
+                     const float *d_sy, float DX, float DY, unsigned long long *cnt, hipStream_t s, uint32_t *d_xrgb)
 {
     using namespace rt::whitted;
     static const int level_blocks = resident_blocks(level_kernel<COUNT>);
     const dim3 tiles((w + 15) / 16, (rows + 15) / 16), block(256);
-    const int qblocks = (int)std::min<long long>(((long long)A.cap + 255) / 256, 2048);
-    hipLaunchKernelGGL(scene_kernel, dim3(1), dim3(64), 0, s, d_prims, nprims, (Scene *)A.scene);
+    const int qblocks = (int)std::min<long long>(((long long)A.pool + 255) / 256, 2048);
     hipLaunchKernelGGL(root_kernel<COUNT>, tiles, block, 0, s, A, row_end, d_sx, d_sy, DX, DY, cnt);
     for (int L = 1; L < LEVELS; L++) {
         hipLaunchKernelGGL(tir_kernel, dim3(64), dim3(64), 0, s, A, L - 1, d_sx, d_sy, DX, DY);
@@ -1030,33 +1112,54 @@ int launch_wavefront(const rt_primitive *d_prims, int nprims, const rt::whitted:
     return rtrt::check_launch("rtw wavefront kernels");
 }
 
-
 int render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int w, int h, int row_begin,
                  int row_end, uint64_t *d_counters, void *stream, bool ocl)
 {
     rtrt::DeviceState *st;
     int rc = rtrt::state(&st);
     if (rc) return rc;
-    const float *d_sx, *d_sy;
-    rc = ocl ? view_tables_ocl(*st, w, h, &d_sx, &d_sy) : view_tables(*st, w, h, &d_sx, &d_sy);
-    if (rc) return rc;
-    const float DX = (3.0f - -3.0f) / w, DY = (-2.25f - 2.25f) / h;    // Engine_InitRender / openCLcode.cl:20-21
-    const int rows = row_end - row_begin;
-    rt::whitted::WfArgs A;
-    const int side = ocl ? 2 : 3;
-    rc = wavefront_arena(*st, w, rows, side * side, &A);
-    if (rc) return rc;
-    A.row_begin = row_begin;
-    A.side = side;
-    A.nsub = side * side;
-    A.ocl = ocl;
+    std::lock_guard<std::recursive_mutex> lk(st->mu);
     hipStream_t s = (hipStream_t)stream;
+    // The arena and view tables belong to the device: order this frame after
+    // the previous one, whatever stream that ran on.
+    if (st->wf_pending) {
+        hipError_t e = hipStreamWaitEvent(s, st->wf_done, 0);
+        if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async wait");
+    }
+    const float DX = (3.0f - -3.0f) / w, DY = (-2.25f - 2.25f) / h;    // Engine_InitRender / openCLcode.cl:20-21
+    const float *d_sx, *d_sy;
+    if ((rc = view_tables(*st, s, w, h, ocl, DX, DY, &d_sx, &d_sy))) return rc;
+    const int rows = row_end - row_begin;
+    const int side = ocl ? 2 : 3, nsub = side * side;
+    const int ngroups = (rows + 15) / 16;                // 16-row groups (slab_row)
+    long long nslab = ((long long)w * ngroups * 16 * nsub + SLAB_TREES - 1) / SLAB_TREES;
+    if (const char *e = getenv("RT_WHITTED_SLABS")) nslab = std::max(1, atoi(e));   // test hook
+    nslab = std::min<long long>(std::max<long long>(nslab, 1), ngroups);
+    const int slab_rows = (int)((ngroups + nslab - 1) / nslab) * 16;
+    rt::whitted::WfArgs A;
+    if ((rc = wavefront_arena(*st, w, slab_rows, nsub, &A))) return rc;
+    A.side = side;
+    A.nsub = nsub;
+    A.ocl = ocl;
+    A.row_stride = (int)nslab;
     unsigned long long *cnt = (unsigned long long *)d_counters;
-    hipError_t e = hipMemsetAsync(A.count, 0, sizeof(int) * rt::whitted::C_TOTAL * rt::whitted::CSTRIDE, s);
-    if (e == hipSuccess) e = hipMemsetAsync(A.fixflag, 0, sizeof(int) * (size_t)A.ntrees, s);
-    if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async memset");
-    if (cnt) return launch_wavefront<true>(d_prims, nprims, A, w, rows, row_end, d_sx, d_sy, DX, DY, cnt, s, d_xrgb);
-    return launch_wavefront<false>(d_prims, nprims, A, w, rows, row_end, d_sx, d_sy, DX, DY, cnt, s, d_xrgb);
+    hipLaunchKernelGGL(rt::whitted::scene_kernel, dim3(1), dim3(64), 0, s, d_prims, nprims, (rt::whitted::Scene *)A.scene);
+    for (int k = 0; k < (int)nslab; k++) {
+        const int srows = (int)((ngroups - k + nslab - 1) / nslab) * 16;
+        A.row_begin = row_begin + 16 * k;
+        A.npix = w * srows;
+        A.ntrees = A.npix * nsub;
+        hipError_t e = hipMemsetAsync(A.count, 0, sizeof(int) * rt::whitted::C_TOTAL * rt::whitted::CSTRIDE, s);
+        if (e == hipSuccess) e = hipMemsetAsync(A.fixbits, 0, sizeof(unsigned) * (((size_t)A.ntrees + 31) / 32), s);
+        if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async memset");
+        rc = cnt ? launch_wavefront<true>(A, w, srows, row_end, d_sx, d_sy, DX, DY, cnt, s, d_xrgb)
+                 : launch_wavefront<false>(A, w, srows, row_end, d_sx, d_sy, DX, DY, cnt, s, d_xrgb);
+        if (rc) return rc;
+    }
+    hipError_t e = hipEventRecord(st->wf_done, s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async record");
+    st->wf_pending = true;
+    return RT_OK;
 }
 
 }  // namespace
@@ -1095,6 +1198,9 @@ extern "C" int rtw_render_ocl(const rt_primitive *prims, int nprims, uint32_t *x
     rtrt::DeviceState *st;
     int rc = rtrt::state(&st);
     if (rc) return rc;
+    std::lock_guard<std::recursive_mutex> lk(st->mu);
+    // slots 0..2 may still feed a frame issued on another stream
+    if (st->wf_pending && (rc = wait_frame(*st))) return rc;
     const size_t frame_bytes = sizeof(uint32_t) * (size_t)w * h;
     void *d_prims, *d_frame, *d_cnt;
     if ((rc = rtrt::scratch(*st, 0, sizeof(rt_primitive) * nprims, &d_prims))) return rc;
@@ -1126,6 +1232,9 @@ extern "C" int rtw_render(const rt_primitive *prims, int nprims, uint32_t *xrgb,
     rtrt::DeviceState *st;
     int rc = rtrt::state(&st);
     if (rc) return rc;
+    std::lock_guard<std::recursive_mutex> lk(st->mu);
+    // slots 0..2 may still feed a frame issued on another stream
+    if (st->wf_pending && (rc = wait_frame(*st))) return rc;
     const size_t frame_bytes = sizeof(uint32_t) * (size_t)w * h;
     void *d_prims, *d_frame, *d_cnt;
     if ((rc = rtrt::scratch(*st, 0, sizeof(rt_primitive) * nprims, &d_prims))) return rc;

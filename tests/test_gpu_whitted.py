@@ -114,3 +114,52 @@ def test_random_scenes_vs_oracle(rt, oracle, seed):
     ref, rc = oracle.whitted_render_ocl(w, h, nthreads=8, prims=P, n=n)
     got, gc = rt.whitted_render_ocl(w, h, prims=P, nprims=n, counters=True)
     assert (got == ref).all() and gc == rc
+
+
+@pytest.mark.parametrize("slabs", [2, 3, 7])
+def test_interleaved_slabs_bit_exact(rt, oracle, slabs, monkeypatch):
+    """The level pass over several interleaved row slabs (what frames above
+    SLAB_TREES trees use) gives the same frame and counts; also with queues
+    small enough to send trees to the fixup pass."""
+    monkeypatch.setenv("RT_WHITTED_SLABS", str(slabs))
+    w, h = 320, 240
+    ref, rc = oracle.whitted_render(w, h, nthreads=8)
+    got, gc = rt.whitted_render(w, h, counters=True)
+    assert (got == ref).all() and gc == rc
+    monkeypatch.setenv("RT_WHITTED_QUEUE_CAP", "3000")
+    got, gc = rt.whitted_render(w, h, counters=True)
+    assert (got == ref).all() and gc == rc
+    ref, rc = oracle.whitted_render_ocl(w, h, nthreads=8)
+    got, gc = rt.whitted_render_ocl(w, h, counters=True)
+    assert (got == ref).all() and gc == rc
+
+
+def test_device_memory_bounded(rt):
+    """The level pass's device arena for a 1920x1080 frame (two slabs of
+    queues at a third of the slab's trees per level) stays near 1.2 GB."""
+    rt.lib().rt_release()
+    rt.whitted_render(1920, 1080)
+    assert rt.lib().rt_cached_bytes() < 1.5e9, rt.lib().rt_cached_bytes()
+
+
+def test_async_frames_on_other_streams_are_ordered(rt, oracle):
+    """Device-resident frames of different sizes issued back to back on two
+    non-blocking streams without host synchronisation: the shared arena and
+    view tables are reused only after the previous frame."""
+    import ctypes as C
+    import torch
+    prims, n = rt.scenes.whitted_scene()
+    dev = torch.device("cuda", 0)
+    d_prims = torch.frombuffer(bytearray(bytes(prims)[:96 * n]), dtype=torch.uint8).to(dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    sizes = [(1920, 1080, s1), (640, 480, s2), (800, 600, s1), (1920, 1080, s2)]
+    frames = [torch.zeros(h * w, dtype=torch.int32, device=dev) for w, h, _ in sizes]
+    torch.cuda.synchronize(dev)
+    for (w, h, s), f in zip(sizes, frames):
+        rt.check(rt.lib().rtw_render_async(d_prims.data_ptr(), n, f.data_ptr(), w, h, 20, h - 70, None,
+                                           C.c_void_p(s.cuda_stream)))
+    torch.cuda.synchronize(dev)
+    for (w, h, _), f in zip(sizes, frames):
+        ref, _ = oracle.whitted_render(w, h, nthreads=8)
+        got = f.cpu().numpy().view(np.uint32).reshape(h, w)
+        assert (got == ref).all(), (w, h)
