@@ -99,8 +99,9 @@ def test_generic_lds_path(rt, oracle):
     _check((f.colors, f.seeds, f.pixels, f.counters), ref)
 
 
-def test_large_scene_global_path(rt, oracle):
-    """configs[4] scene (10k spheres: above the LDS budget -> global SoA path)."""
+def test_large_scene_hierarchy_vs_oracle(rt, oracle):
+    """configs[4] scene (10k spheres, >= 256: the exact-culling hierarchy
+    path) against the oracle's full scan, small frame."""
     spheres, n, cam = rt.scenes.complex10k()
     w, h = 48, 32
     rt.scenes.update_camera(cam, w, h)
@@ -108,6 +109,48 @@ def test_large_scene_global_path(rt, oracle):
     f.render(1)
     ref = _oracle_frame(oracle, w, h, [1], spheres=(spheres, n), cam=cam)
     _check((f.colors, f.seeds, f.pixels, f.counters), ref)
+
+
+@pytest.mark.parametrize("env", [{"RT_SPT_NO_BVH": "1"}, {"RT_SPT_GEO": "global"}])
+def test_large_scene_global_path(rt, oracle, env, monkeypatch):
+    """The global-SoA full-scan kernel (GEO_GLOBAL: scenes above the LDS
+    budget without the hierarchy, or forced for any scene) vs the oracle:
+    the 10k configs[4] scene with the hierarchy disabled, and Cornell."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    if "RT_SPT_NO_BVH" in env:
+        spheres, n, cam = rt.scenes.complex10k()
+        w, h = 32, 24
+        rt.scenes.update_camera(cam, w, h)
+    else:
+        (spheres, n), w, h = rt.scenes.cornell(), 96, 64
+        cam = rt.scenes.cornell_camera(w, h)
+    f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n, camera=cam)
+    f.render(2)
+    ref = _oracle_frame(oracle, w, h, [2], spheres=(spheres, n), cam=cam)
+    _check((f.colors, f.seeds, f.pixels, f.counters), ref)
+
+
+@pytest.mark.parametrize("counted", [True, False])
+def test_configs4_full_size_golden(rt, oracle, counted):
+    """BASELINE configs[4] at full size -- the 10k-sphere scene_build_complex
+    scene, 1920x1080, 64 spp from the initial state -- through the hierarchy
+    kernel (with and without the work counters), against the golden hashes of
+    the reference's own full-scan core (tests/golden/make_golden_c4.py,
+    oracle/_ref: geomfunc.h:71-110 Intersect / IntersectP)."""
+    import json
+    import os
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
+    g = gold["smallpt"]["1920x1080_64spp_complex10k"]
+    spheres, n, cam = rt.scenes.complex10k()
+    w, h = 1920, 1080
+    rt.scenes.update_camera(cam, w, h)
+    f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n, camera=cam)
+    f.render(64, counters=counted)
+    got = (oracle.fnv1a64(f.colors), oracle.fnv1a64(f.pixels), oracle.fnv1a64(f.seeds))
+    assert got == (g["colors"], g["pixels"], g["seeds"])
+    if counted:
+        assert f.counters[3] == w * h * 64
 
 
 def test_async_device_paths(rt, oracle):
