@@ -301,12 +301,11 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
     const float dy = fabsf(r.d.y) < 1e-30f ? copysignf(1e-30f, r.d.y) : r.d.y;
     const float dz = fabsf(r.d.z) < 1e-30f ? copysignf(1e-30f, r.d.z) : r.d.z;
     const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
-    const float ax = fabsf(ix), ay = fabsf(iy), az = fabsf(iz);
     const float e = fabsf(r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z - 1.f);
     const float alpha = e < 0x1p-16f ? BVH_K * (1.04e-3f + __builtin_amdgcn_sqrtf(e + 0x1p-22f)) : 1e30f;
-    // Layout of this ray's direction octant: near children first.
-    const float4 *nodes = B.node + 2 * (size_t)B.nnodes *
-                                       ((dx < 0.f ? 1 : 0) | (dy < 0.f ? 2 : 0) | (dz < 0.f ? 4 : 0));
+    // Layout of this ray's direction octant: near children first.  A 32-bit
+    // element offset from the uniform base (one VGPR, not a 64-bit pointer).
+    const unsigned lay = 2u * (unsigned)B.nnodes * ((dx < 0.f ? 1u : 0u) | (dy < 0.f ? 2u : 0u) | (dz < 0.f ? 4u : 0u));
     // Crossed leaves are postponed: a lane that reaches one stops stepping
     // and keeps it pending; the wave tests the pending leaves' spheres
     // together once at least RT_BVH_BATCH/64 of its lanes still in the walk
@@ -319,14 +318,14 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
         if (node < B.nnodes && pend == 0) {
             BVH_ST(0, 1);
             BVH_ST_WAVE(3);
-            const float4 a = nodes[2 * node], b = nodes[2 * node + 1];
+            const float4 a = B.node[lay + 2u * (unsigned)node], b = B.node[lay + 2u * (unsigned)node + 1u];
             const int link = __float_as_int(a.w);
             const float lim = shadow ? maxt : t;
             const float cx = a.x - r.o.x, cy = a.y - r.o.y, cz = a.z - r.o.z;
             const float dist = __builtin_amdgcn_sqrtf(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, cz * cz)));
             const float m = __builtin_fmaf(alpha, dist, b.w);
             const float tcx = cx * ix, tcy = cy * iy, tcz = cz * iz;                // slab centres
-            const float hx = (b.x + m) * ax, hy = (b.y + m) * ay, hz = (b.z + m) * az;  // slab half-widths
+            const float hx = (b.x + m) * fabsf(ix), hy = (b.y + m) * fabsf(iy), hz = (b.z + m) * fabsf(iz);  // slab half-widths
             const float tn = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
             const float tf = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
             const bool cross = tn <= tf && tf >= 0.f && tn <= lim;
@@ -353,13 +352,9 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
             BVH_ST(2, c);
             BVH_ST_WAVE(4);
             float4 g[BVH_LEAF_MAX];
-            int gi[BVH_LEAF_MAX];
 #pragma unroll
-            for (int q = 0; q < BVH_LEAF_MAX; q++) {      // all loads first: one latency per leaf
-                const int j = f + (q < c ? q : 0);
-                g[q] = B.geo[j];
-                gi[q] = B.id[j];
-            }
+            for (int q = 0; q < BVH_LEAF_MAX; q++)        // all loads first: one latency per leaf
+                g[q] = B.geo[f + (q < c ? q : 0)];
 #if RT_BVH_LEAF_BF
             // Branch-free sphere tests (as query_bf): sqrt_nr is exact for det
             // in [2^-96, inf) and NaN below 0 (a miss); a wave with a lane
@@ -380,25 +375,41 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
 #pragma unroll
                 for (int q = 0; q < BVH_LEAF_MAX; q++) dq[q] = sphere_hit(g[q], r);
             }
+            // The spheres' reference indices are not loaded with the leaf
+            // (four VGPRs less across the walk): the leaf's new best is kept
+            // as its hierarchy position and its index loaded once, after the
+            // tests; only ties (and the counted any-hit's highest occluder)
+            // load an index on the spot.
+            int bpos = -1;
 #pragma unroll
             for (int q = 0; q < BVH_LEAF_MAX; q++) {
                 if (q < c) {
                     const float d = dq[q];
-                    const int i = gi[q];
                     if (shadow) {
-                        if (d < maxt && i > id) id = i;
-                    } else if (d < t || (d == t && i > id)) {
+                        if (d < maxt) {
+                            if (COUNT) {
+                                const int i = B.id[f + q];
+                                if (i > id) id = i;
+                            } else {
+                                bpos = f + q;
+                            }
+                        }
+                    } else if (d < t) {
                         t = d;
-                        id = i;
+                        bpos = f + q;
+                    } else if (d == t) {
+                        const int cur = bpos >= 0 ? B.id[bpos] : id;
+                        if (B.id[f + q] > cur) bpos = f + q;
                     }
                 }
             }
+            if (bpos >= 0) id = B.id[bpos];
 #else
 #pragma unroll
             for (int q = 0; q < BVH_LEAF_MAX; q++) {
                 if (q < c) {
                     const float d = sphere_hit(g[q], r);
-                    const int i = gi[q];
+                    const int i = B.id[f + q];
                     if (shadow) {
                         if (d < maxt && i > id) id = i;
                     } else if (d < t || (d == t && i > id)) {
@@ -419,7 +430,7 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
     W.pend = pend;
 #ifdef RT_BVH_STATS
     {
-        const float4 a0 = nodes[0], b0 = nodes[1];
+        const float4 a0 = B.node[lay], b0 = B.node[lay + 1u];
         const bool far = fabsf(r.o.x - a0.x) > b0.x || fabsf(r.o.y - a0.y) > b0.y || fabsf(r.o.z - a0.z) > b0.z;
         st[7] = W.node >= B.nnodes && st[0] >= 128; st[8] = st[0] >= 512; st[9] = st[0] >= 2048;
         st[10] = far ? st[0] : 0; st[11] = far; st[12] = shadow; st[13] = shadow ? st[0] : 0;
@@ -488,8 +499,11 @@ __device__ __forceinline__ int to_int(float x)
 #endif
 constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2;
 
+#ifndef RT_BVH_MINWAVES_COUNT
+#define RT_BVH_MINWAVES_COUNT 4   // the counted hierarchy kernels (not timed): room for the counters, no spills
+#endif
 template <bool DL, bool COUNT, int GEO>
-__global__ void __launch_bounds__(1024, GEO == 2 ? RT_BVH_MINWAVES : RT_SPT_MINWAVES)
+__global__ void __launch_bounds__(1024, GEO == 2 ? (COUNT ? RT_BVH_MINWAVES_COUNT : RT_BVH_MINWAVES) : RT_SPT_MINWAVES)
 render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,
               uint32_t *seeds_out, uint32_t *__restrict__ pixels, int w, int h,

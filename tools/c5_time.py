@@ -50,14 +50,17 @@ if stats:
               bs[7], bs[8], bs[9], bs[5], bs[11], bs[10] / max(bs[11], 1), bs[14], bs[12], bs[13] / max(bs[12], 1)))
     print("  alpha > 1/128: %d queries, %.1f nodes each, %d >= 512; origin > 8 root radii away: %d queries, "
           "%.1f nodes each, %d >= 512" % (bs[15], bs[16] / max(bs[15], 1), bs[20], bs[17], bs[18] / max(bs[17], 1), bs[19]))
-a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-a.record(st)
-run()
-b.record(st)
-torch.cuda.synchronize()
-ms = a.elapsed_time(b)
-print("c5 %dx%d spp=%d spheres=%d: %.1f ms, rays %d, %.1f Mrays/s, sphere tests %d" % (
-    W, H, SPP, n, ms, rays, rays / ms / 1e3, int(cnt[2])))
+ts = []
+for _ in range(int(os.environ.get("REPS", "1"))):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    run()
+    b.record(st)
+    torch.cuda.synchronize()
+    ts.append(a.elapsed_time(b))
+ms = float(np.median(ts))
+print("c5 %dx%d spp=%d spheres=%d: %.2f ms (median of %d, min %.2f), rays %d, %.1f Mrays/s, sphere tests %d" % (
+    W, H, SPP, n, ms, len(ts), min(ts), rays, rays / ms / 1e3, int(cnt[2])))
 if int(cnt[7]):
     q = rays
     print("  per query: %.1f nodes, %.1f sphere tests; lane trips / (64 x wave trips) = %.3f" % (
