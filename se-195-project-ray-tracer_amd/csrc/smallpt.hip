@@ -162,6 +162,59 @@ __device__ __forceinline__ int query_bf(const G &geo, const ray3 &r, float &t, i
     return id;
 }
 
+// Two queries in one pass over the spheres (single-light scenes, see
+// render_kernel<..., DUAL>): the path ray's nearest hit (t = 1e20f on entry,
+// as query_bf) and, for lanes with sh set, the pending shadow ray's any hit
+// (ts = maxt on entry; "some update happened" = IntersectP true, the first
+// update = its early-exit index for the test counter).  Each sphere record
+// is loaded once for both rays, and the two dependency chains interleave.
+template <bool COUNT, class G>
+__device__ __forceinline__ void query2_bf(const G &geo, const ray3 &r, float &t, int &id, const ray3 &rs, bool sh,
+                                          float &ts, int &ids, int &firsts)
+{
+    const float t_in = t, ts_in = ts;
+    int first = -1;
+    id = -1;
+    ids = -1;
+    bool bad = false;
+#pragma unroll RT_SPT_QUNROLL
+    for (int i = geo.count() - 1; i >= 0; i--) {
+        const float4 g = geo.at(i);
+        {
+            const float opx = g.x - r.o.x, opy = g.y - r.o.y, opz = g.z - r.o.z;
+            const float b = opx * r.d.x + opy * r.d.y + opz * r.d.z;
+            const float det = b * b - (opx * opx + opy * opy + opz * opz) + g.w;
+            bad = bad || fabsf(det) < 0x1p-96f;
+            const float sd = sqrt_nr(det);
+            const float t1 = b - sd, t2 = b + sd;
+            const float d = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
+            const bool take = d < t;
+            t = take ? d : t;
+            id = take ? i : id;
+        }
+        {
+            const float opx = g.x - rs.o.x, opy = g.y - rs.o.y, opz = g.z - rs.o.z;
+            const float b = opx * rs.d.x + opy * rs.d.y + opz * rs.d.z;
+            const float det = b * b - (opx * opx + opy * opy + opz * opz) + g.w;
+            bad = bad || (sh && fabsf(det) < 0x1p-96f);
+            const float sd = sqrt_nr(det);
+            const float t1 = b - sd, t2 = b + sd;
+            const float d = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
+            const bool take = d < ts;
+            ts = take ? d : ts;
+            ids = take ? i : ids;
+            if (COUNT) firsts = (firsts < 0 && take) ? i : firsts;
+        }
+    }
+    if (wave_any(bad)) {
+        t = t_in;
+        id = query<COUNT>(geo, r, t, first);
+        ts = ts_in;
+        firsts = -1;
+        ids = query<COUNT>(geo, rs, ts, firsts);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Bounding-volume hierarchy for large scenes (BASELINE configs[4]: 10k
 // spheres).  The reference tests every sphere for every ray (geomfunc.h:71-
@@ -502,7 +555,14 @@ constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2;
 #ifndef RT_BVH_MINWAVES_COUNT
 #define RT_BVH_MINWAVES_COUNT 4   // the counted hierarchy kernels (not timed): room for the counters, no spills
 #endif
-template <bool DL, bool COUNT, int GEO>
+// DUAL (path tracing, full-scan geometry, scenes with exactly one light): a
+// DIFF vertex builds its light sample's shadow ray AND its bounce ray in the
+// same iteration -- SampleLights' draws do not depend on the shadow test, so
+// the bounce's draws follow them in the reference's order either way -- and
+// the next iteration queries both (query2_bf) and applies the shadow result
+// (rad += thr * Ld, geomfunc.h:229-230) before it shades the bounce's hit.
+// One iteration per path vertex instead of two for a lit DIFF vertex.
+template <bool DL, bool COUNT, int GEO, bool DUAL = false>
 __global__ void __launch_bounds__(1024, GEO == 2 ? (COUNT ? RT_BVH_MINWAVES_COUNT : RT_BVH_MINWAVES) : RT_SPT_MINWAVES)
 render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,
@@ -578,7 +638,9 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         v3 rad = mk(0.f, 0.f, 0.f), thr = mk(1.f, 1.f, 1.f);
         int depth = 0;
         bool specular = true;
-        bool shadow = false;   // ray is the shadow ray of light li
+        bool shadow = false;   // ray is the shadow ray of light li (DUAL: a shadow ray (hit, sdir) is pending)
+        v3 sdir = mk(0.f, 0.f, 0.f);   // DUAL: the pending shadow ray's direction (origin: hit)
+        bool fin = false;      // DUAL: the sample ends once its pending shadow ray is resolved
         v3 hit, nl;            // the last hit point and its oriented normal (SampleLights' args)
         v3 lsum;               // SampleLights' running result
         float lmax = 0.f;      // shadow ray maxt (len - EPSILON)
@@ -657,10 +719,37 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
 #ifdef RT_SPT_TRACE
             tr_iters++;
 #endif
-            float t = shadow ? lmax : 1e20f;
+            float t = (shadow && !DUAL) ? lmax : 1e20f;
             int first = -1;
             int id;
-            if constexpr (GEO == GEO_BVH) {
+            bool done = false, lights = false, a_R = false;
+            if constexpr (DUAL) {
+                // Both rays at once when any lane holds a shadow ray; its
+                // result is applied first (the light sample precedes the
+                // bounce's hit in the reference's order).
+                if (wave_any(shadow)) {
+                    float ts = lmax;
+                    int ids, firsts = -1;
+                    ray3 rs;
+                    rs.o = hit;
+                    rs.d = sdir;
+                    query2_bf<COUNT>(geo, ray, t, id, rs, shadow, ts, ids, firsts);
+                    if (shadow) {                               // :154-161, then :229-230
+                        SPT_PROF(PB_SHADOW);
+                        cnt.isectp++;
+                        cnt.tests += firsts >= 0 ? (unsigned)(S.n - firsts) : (unsigned)S.n;
+                        if (ids < 0) {
+                            const float4 le = S.lrec[2];
+                            const v3 ld = vsmul(lw, mk(le.x, le.y, le.z));   // 0 + e * s
+                            rad = vadd(rad, vmul(thr, ld));
+                        }
+                        shadow = false;
+                        done = fin;
+                    }
+                } else {
+                    id = query_bf<COUNT>(geo, ray, t, first);
+                }
+            } else if constexpr (GEO == GEO_BVH) {
                 // Resumable walk: a lane whose query needs more than this
                 // iteration's step budget sits out the rest of the iteration
                 // and continues its walk in the next one.
@@ -677,9 +766,10 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 id = query<COUNT>(geo, ray, t, first);
 #endif
             }
-            bool done = false, lights = false, a_R = false;
             float dp = 0.f, inv_sign = 1.f;  // REFR (pass A): vdot(normal, ray.d), -1 * sign(dp); and id
-            if (shadow) {                                       // :154-161
+            if (DUAL && fin) {
+                // the path ended at the last DIFF vertex: no path ray this iteration
+            } else if (shadow && !DUAL) {                       // :154-161
                 SPT_PROF(PB_SHADOW);
                 cnt.isectp++;
                 cnt.tests += first >= 0 ? (unsigned)(S.n - first) : (unsigned)S.n;
@@ -817,12 +907,17 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     const float quo = num / den;
                     if (!with_r || a_L) {
                         if (lit) {
-                            ray.o = hit;
-                            ray.d = vn;
+                            if (DUAL) {
+                                sdir = vn;                      // queried next iteration, with the bounce ray
+                            } else {
+                                ray.o = hit;
+                                ray.d = vn;
+                            }
                             lmax = len - EPS;
                             lw = quo;
                             shadow = true;
                             a_L = false;
+                            if (DUAL) lights_done = true;       // the only light
                         } else {
                             li++;
                             a_L = li < S.nlights;
@@ -851,13 +946,16 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             }
             if (was_R) done = depth > 6;
             if (lights_done) {                                  // :229-230, then the bounce
-                rad = vadd(rad, vmul(thr, lsum));
+                // (DUAL: Ld is 0 + e * s once the pending shadow ray is
+                // resolved, or 0 -- and rad + thr * 0 == rad -- if none.)
+                if (!DUAL) rad = vadd(rad, vmul(thr, lsum));
                 if (DL) {
                     done = true;                                // :413-414
                 } else if (depth > 6) {                         // the bounce's two draws, then :184
                     (void)get_random(s0, s1);
                     (void)get_random(s0, s1);
-                    done = true;
+                    if (DUAL && shadow) fin = true;             // ends after the shadow result
+                    else done = true;
                 } else {
                     need_bounce = true;
                 }
@@ -877,6 +975,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 cnt.samples++;
                 k++;
                 need_cam = k < nsamples;
+                fin = false;
             }
         }
         if (nsamples > 0) {
@@ -977,7 +1076,7 @@ Shape launch_shape(const spt_scene &sc, int w, int r0, int r1)
     return g;
 }
 
-template <bool DL, bool COUNT, int GEO>
+template <bool DL, bool COUNT, int GEO, bool DUAL = false>
 void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &cam, float *colors,
             const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h, int r0, int r1,
             int first, int ns, unsigned long long *cnt)
@@ -987,7 +1086,7 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     const float4 *gg = sc.d_soa, *ge = gg + n, *gc = ge + n, *gl = gc + n;
     size_t lds = LDS ? (size_t)(3 * n + 3 * sc.nlights) * sizeof(float4) : 0;
     if (g.wpb == 16 && lds < 81 * 1024) lds = 81 * 1024;   // > half the CU's 160 KiB: one block per CU
-    hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
+    hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, first,
                        ns, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt);
 }
@@ -997,9 +1096,20 @@ void launch_mode(bool dl, bool count, const Shape &grid, hipStream_t s, const sp
                  float *colors, const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h,
                  int r0, int r1, int first, int ns, unsigned long long *cnt)
 {
+    // The two-query iteration for path tracing in single-light scenes, for
+    // windows of at most four waves per SIMD (a multi-GPU row band: the 16-
+    // wave block shape), where per-wave ILP is what is short: N = 8 band
+    // 2.87 -> 2.78 ms.  At full occupancy its 94 VGPRs (occupancy 5 instead
+    // of 6) cost more than the saved iterations: full frame 19.0 -> 19.6 ms.
+    // RT_SPT_DUAL=0 / 1 forces it off / on (A/B).
+    const int dual_env = getenv("RT_SPT_DUAL") ? atoi(getenv("RT_SPT_DUAL")) : -1;
+    const bool dual_ok = dual_env < 0 ? grid.wpb == 16 : dual_env != 0;
     if (dl) {
         if (count) launch<true, true, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
         else launch<true, false, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+    } else if (GEO != rt::smallpt::GEO_BVH && sc.nlights == 1 && dual_ok) {
+        if (count) launch<false, true, GEO, true>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+        else launch<false, false, GEO, true>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
     } else {
         if (count) launch<false, true, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
         else launch<false, false, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);

@@ -301,3 +301,27 @@ def test_pack_pixels_matches_render(rt):
     torch.cuda.synchronize()
     got = px.cpu().numpy().view(np.uint32).reshape(h, w)
     assert (got[50:120] == f.pixels.reshape(h, w)[50:120]).all() and not got[:50].any() and not got[120:].any()
+
+
+@pytest.mark.parametrize("dual", ["0", "1"])
+def test_one_and_two_query_iterations(rt, oracle, dual, monkeypatch):
+    """Both forms of the single-light loop -- one ray query per iteration, and
+    the two-query iteration (shadow ray + bounce ray together, which the
+    library picks for multi-GPU row bands) -- forced either way, against the
+    oracle at a small size and the reference-core golden at 1920x1080x64."""
+    import json
+    import os
+    monkeypatch.setenv("RT_SPT_DUAL", dual)
+    w, h = 200, 150
+    f = rt.SmallptFrame(w, h)
+    f.render(3)
+    f.render(2, counters=False)
+    ref = _oracle_frame(oracle, w, h, [3, 2])
+    assert (f.colors.view(np.uint32) == ref[0].view(np.uint32)).all()
+    assert (f.seeds == ref[1]).all() and (f.pixels == ref[2]).all()
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
+    g = g["smallpt"]["1920x1080_64spp"]
+    f = rt.SmallptFrame(1920, 1080)
+    f.render(64, counters=False)
+    assert (oracle.fnv1a64(f.colors), oracle.fnv1a64(f.pixels), oracle.fnv1a64(f.seeds)) == \
+        (g["colors"], g["pixels"], g["seeds"])
