@@ -13,6 +13,10 @@
  *     and the buffer traffic of UpdateRenderingGPU (:642-782) / ReInit*GPU
  *     (:784-830), computing UpdateRenderingCPU's per-pixel result
  *     (smallptCPU.cpp:84-123: flipped colour/seed slot, running average, toInt).
+ *   Queue tracer (Raytracer3.2.03): rtq_* replace raytracer_non_kernel
+ *     (raytracer_non_OpenCL.c:285-449), the CPU twin its raytracer.c:756
+ *     calls in place of run_openCL_kernel (:417-640), computing its uchar4
+ *     frame bit for bit.
  *
  * Plain pointers and sizes only.  Every entry point returns RT_OK (0) or a
  * negative RT_ERR_* code; rt_last_error() describes the last failure of the
@@ -60,6 +64,21 @@ typedef struct {
     rt_vec3 orig, target;
     rt_vec3 dir, x, y;
 } rt_camera;
+
+/* Raytracer3.2.03 raytracer_non_OpenCL.c:42-44 float_4 */
+typedef struct { float x, y, z, w; } rtq_float4;
+
+/* Raytracer3.2.03 raytracer_non_OpenCL.c:67-81 Primitive_2 -- 96 bytes
+ * (the C++ bool is_light is one byte). */
+typedef struct {
+    rtq_float4 m_color;
+    float m_refl, m_diff, m_refr, m_refr_index, m_spec, dummy_3;
+    int32_t type;                 /* PLANE = 0, SPHERE = 1 */
+    uint8_t is_light;
+    uint8_t pad_[3];
+    rtq_float4 normal, center;
+    float depth, radius, sq_radius, r_radius;
+} rtq_primitive;
 
 /* ------------------------------------------------------------ runtime */
 const char *rt_last_error(void);
@@ -212,6 +231,24 @@ int spt_render_multi(const rt_sphere *spheres, unsigned nspheres, const rt_camer
                      float *colors, uint32_t *seeds, uint32_t *pixels, int w, int h,
                      int first_sample, int nsamples, int mode, uint64_t *counters,
                      const int *devices, int ngpus);
+
+/* ------------------------------------------------------------ queue tracer (3.2.03) */
+/* Blocking, host buffers, whole frame: raytracer_non_kernel(pixels, w, h,
+ * prims, nprims) (raytracer_non_OpenCL.c:285-449).  pixels: w*h uchar_4
+ * (r, g, b, 0) row-major -- as uint32, r | g<<8 | b<<16.  counters (nullable,
+ * host, 4 x u64): rays traced (raytrace calls), shadow rays, intersect calls,
+ * undefined-behaviour events.  The last counts what the reference leaves
+ * undefined and this library defines as "no child rays": a ray at depth < 5
+ * that hits nothing (the reference then reads primitives[-1], :373) or hits a
+ * light with m_refl or m_refr > 0 (point_intersect is uninitialised, :197).
+ * Neither occurs in the reference scene (scene.c:53-97). */
+int rtq_render(const rtq_primitive *prims, int nprims, uint32_t *pixels, int w, int h,
+               uint64_t *counters);
+/* Asynchronous, device-resident: rows [row_begin,row_end) of the w x h frame
+ * (0 <= row_begin < row_end <= h; other rows untouched) into d_pixels (w*h);
+ * d_counters: device u64[4] accumulated into (nullable). */
+int rtq_render_async(const rtq_primitive *d_prims, int nprims, uint32_t *d_pixels, int w, int h,
+                     int row_begin, int row_end, uint64_t *d_counters, void *stream);
 
 /* Host helper: AllocateBuffers' seed fill (smallptGPU.cpp:105-110) --
  * srand(seed); seeds[i] = max(rand(), 2) for i < n, with the host libc's

@@ -9,6 +9,8 @@
  *
  *   Whitted : raytracer3.0.06.no_rec.samp/scene.cpp + raytracer.cpp
  *   smallpt : smallptgpu-v1.6/geomfunc.h + smallptCPU.cpp + displayfunc.cpp
+ *   queue   : Raytracer3.2.03/raytracer/OpenCL Raytracer/raytracer_non_OpenCL.c
+ *             + scene.c (the 3.2.x queue tracer's CPU path)
  *
  * Parity pin: SURVEY.md §8(c) known-answer hashes produced by the reference
  * itself (tests/golden/known_answers.json) plus oracle/_ref builds of the
@@ -18,6 +20,7 @@
  *   Primitive 96 B  raytracer.h:23-32 (+ Material :18-21, plane common.h:49-53)
  *   Sphere    44 B  smallptgpu-v1.6/geom.h:43-47
  *   Camera    60 B  smallptgpu-v1.6/camera.h:29-34
+ *   Primitive_2 96 B Raytracer3.2.03/.../raytracer_non_OpenCL.c:67-81
  */
 #ifndef RT_ORACLE_H
 #define RT_ORACLE_H
@@ -103,6 +106,31 @@ void ors_render(const or_sphere *s, unsigned n, const or_camera *cam,
  * writes up to cap spheres in the Perl script's emission order, returns the
  * number it would emit. */
 int  ors_hypersphere(or_sphere *out, int cap, double max_depth);
+
+/* ---------------- queue tracer (Raytracer3.2.03) ---------------- */
+
+typedef struct { float x, y, z, w; } orq_f4;       /* float_4, raytracer_non_OpenCL.c:42-44 */
+
+/* Primitive_2, raytracer_non_OpenCL.c:67-81 (bool is_light: one byte) */
+typedef struct {
+    orq_f4  m_color;
+    float   m_refl, m_diff, m_refr, m_refr_index, m_spec, dummy_3;
+    int32_t type;          /* prim_type: PLANE=0, SPHERE=1 */
+    uint8_t is_light;
+    uint8_t pad_[3];
+    orq_f4  normal, center;
+    float   depth, radius, sq_radius, r_radius;
+} orq_primitive;
+
+/* create_scene (scene.c:48-97, CHOOSE_SCENE 0) after raytracer.c:721-746's
+ * copy into Primitive_2; returns 17. */
+int  orq_scene_init(orq_primitive *out, int cap);
+/* raytracer_non_kernel (raytracer_non_OpenCL.c:285-449) over rows
+ * [row_begin,row_end) of the w x h frame; pixels: uchar_4 (r,g,b,0) per pixel.
+ * counters (nullable): [0] rays traced (raytrace calls)  [1] shadow rays
+ *   [2] intersect calls  [3] undefined-behaviour events (see queue_oracle.c). */
+void orq_render(const orq_primitive *P, int n, uint8_t *pixels, int w, int h, int row_begin, int row_end,
+                uint64_t *counters, int nthreads);
 
 /* FNV-1a-64 over bytes, as used for the SURVEY.md §8(c) known answers. */
 uint64_t or_fnv1a64(const void *data, size_t nbytes);

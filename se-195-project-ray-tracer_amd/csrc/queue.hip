@@ -1,0 +1,848 @@
+// queue.hip -- gfx950 kernels for the Raytracer3.2.03 queue tracer.
+//
+// Computes, bit for bit, what raytracer_non_kernel
+// (Raytracer3.2.03/raytracer/OpenCL Raytracer/raytracer_non_OpenCL.c:285-449,
+// the CPU twin raytracer.c:756 calls instead of its OpenCL kernel) writes:
+// per pixel 3x3 primary sub-samples (:317-318), each expanded by a FIFO ray
+// queue (:30-40) into a breadth-first tree of reflected and refracted rays to
+// depth 5 (:370-432), every ray's colour added to the pixel's accumulator AS
+// IT IS POPPED (:351-368) -- weighted by its own weight, transparency and
+// (reflected rays) the colour of the primitive it left -- and the sum packed
+// as uchar4 (r, g, b, 0) with the x(256/9) scale and 255 clamp (:436-447).
+//
+// Differences from raytracer3.0.06 (whitted.hip) that shape the kernels: no
+// back-accumulation up the tree (a node's term is final when it is traced),
+// no stale refraction ray (total internal reflection just queues nothing),
+// and the pixel's sum is one sequential float chain over all its nodes in
+// queue order: tree 0's nodes in BFS order, then tree 1's, ...  The BFS order
+// of a tree is heap order (node i's children are 2i+1 reflected, 2i+2
+// refracted, pushed in that order, :371-431).
+//
+// Mapping (MI355X-first):
+//   * level-synchronous trees (rt_levelq.h queues): root_kernel traces the 9
+//     primary rays of every pixel (one coherent launch, a lane = a pixel),
+//     level_kernel L = 1..5 traces one level of every tree from a compacted
+//     queue; each node's term (3 floats) and child slots are recorded;
+//   * final_kernel folds each pixel's chain in the reference's order: the
+//     leading trees without children were already summed by root_kernel, the
+//     rest are walked breadth-first through their child links (a 32-slot
+//     per-lane ring in LDS holds pool slots, not rays);
+//   * a tree with a node that did not fit the pool is re-evaluated in
+//     final_kernel itself, node by node in heap order, each node's ray
+//     re-derived from the root (registers only, no per-lane ray queue);
+//   * the <= 64 primitives are staged per block into LDS as per-type SoA;
+//   * the reference's libm: sqrt -> correctly rounded sqrtf, exp(float) ->
+//     glibc expf, pow(float, 20) -> glibc's double pow (g++'s promoting
+//     std::pow), all restated bit-exactly in rt_glibc_math.h.
+#include "rt_common.h"
+#include "rt_glibc_math.h"
+#include "rt_levelq.h"
+
+namespace rt {
+namespace queue {
+
+constexpr int MAXP = 64;        // raytracer.c:720 allocates 50 Primitive_2
+constexpr int LEVELS = 6;       // depths 0..5 (TRACEDEPTH 5, :4)
+constexpr int NSUB = 9;         // 3 x 3 sub-samples (:317-318)
+constexpr float EPS = 0.001f;   // :26
+constexpr int PLANE = 0, SPHERE = 1;
+constexpr int RING = 32;        // BFS ring per lane in final_kernel (a level-4 node
+                                // leaves at most 32 level-5 slots queued)
+
+struct Scene {
+    // Dense per-type geometry for the nearest-hit loop (ties resolved to the
+    // lowest primitive index, as the reference's strict '<' over ascending s).
+    float4 sph[MAXP];     // centre.xyz, sq_radius
+    float4 pln[MAXP];     // normal.xyz, depth
+    int sph_id[MAXP], pln_id[MAXP];
+    // Non-light primitives (the shadow loop's occluders, :232-240) and their
+    // position in the reference's loop (for the test counter).
+    float4 osph[MAXP], opln[MAXP];
+    int osph_pos[MAXP], opln_pos[MAXP];
+    // Per primitive, for per-lane lookups of the hit primitive.
+    float4 col[MAXP];     // m_color.xyz, m_refl
+    float4 mat[MAXP];     // m_refr, m_refr_index, m_diff, m_spec
+    float4 geo[MAXP];     // sphere: centre.xyz, r_radius   plane: normal.xyz
+    float4 cen[MAXP];     // center.xyz (the light position of :215-217)
+    int type[MAXP];
+    int light[MAXP];
+    int lights[MAXP];     // is_light primitives, in index order
+    int n, ns, np, nos, nop, nlights, nnonlight, pad_;
+};
+
+// One queued ray (Ray, :83-92): what its trace and its term need.
+struct Node {
+    ray3 r;
+    float w;              // weight
+    v3 tr;                // transparency
+    int origin;           // origin_primitive (REFLECTED: its colour scales the term)
+    int type;             // ORIGIN 0, REFLECTED 1, REFRACTED 2
+    int rcode;            // r_index: 0 = 1.0f, k > 0 = m_refr_index of primitive k-1
+};
+
+struct Hit {
+    v3 col;               // ray_col
+    v3 pi;                // point_intersect
+    int prim;             // -1: no hit
+    int result;           // HIT 1 / INPRIM -1
+    float dist;
+    unsigned cnt;         // tests | shadow rays << 16 (work counters)
+};
+
+// Sphere half of intersect (:111-148): the candidate distance (INPRIM: i2,
+// HIT: i1) or +inf with res = 0.
+__device__ __forceinline__ float sphere_cand(float4 g, const ray3 &r, int &res)
+{
+    const float vx = r.o.x - g.x, vy = r.o.y - g.y, vz = r.o.z - g.z;
+    float b = vx * r.d.x + vy * r.d.y + vz * r.d.z;
+    b = -b;
+    const float det = (b * b) - (vx * vx + vy * vy + vz * vz) + g.w;
+    res = 0;
+    float cand = __builtin_inff();
+    if (det > 0) {
+        const float sq = sqrt_exact(det);
+        const float i1 = b - sq, i2 = b + sq;
+        if (i2 > 0) {
+            cand = i1 < 0 ? i2 : i1;
+            res = i1 < 0 ? -1 : 1;
+        }
+    }
+    return cand;
+}
+
+// plane_intersect, :95-109.
+__device__ __forceinline__ float plane_cand(float4 g, const ray3 &r)
+{
+    const float d = g.x * r.d.x + g.y * r.d.y + g.z * r.d.z;
+    float cand = __builtin_inff();
+    if (d != 0) {
+        const float t = -((g.x * r.o.x + g.y * r.o.y + g.z * r.o.z) + g.w) / d;
+        if (t > 0) cand = t;
+    }
+    return cand;
+}
+
+// get_normal, :162-177.
+__device__ __forceinline__ v3 normal_at(const Scene &S, int p, v3 pt)
+{
+    const float4 g = S.geo[p];
+    const int t = S.type[p];
+    if (t == SPHERE) return mk((pt.x - g.x) * g.w, (pt.y - g.y) * g.w, (pt.z - g.z) * g.w);
+    if (t == PLANE) return mk(g.x, g.y, g.z);
+    return mk(0.f, 0.f, 0.f);
+}
+
+// raytrace, :179-281.
+template <bool COUNT>
+__device__ Hit trace(const Scene &S, const ray3 &ray)
+{
+    Hit h;
+    h.col = mk(0.f, 0.f, 0.f);
+    h.pi = mk(0.f, 0.f, 0.f);
+    h.result = 1;
+    // :181-193 nearest hit below 1e7, lowest index on ties.
+    float dist = 10000000.0f;
+    int prim = -1, result = 1;
+    for (int k = 0; k < S.ns; k++) {
+        int res;
+        const float c = sphere_cand(S.sph[k], ray, res);
+        const int id = S.sph_id[k];
+        if (res && (c < dist || (c == dist && prim >= 0 && id < prim))) { dist = c; prim = id; result = res; }
+    }
+#pragma unroll 4
+    for (int k = 0; k < S.np; k++) {
+        const float c = plane_cand(S.pln[k], ray);
+        const int id = S.pln_id[k];
+        if (c < dist || (c == dist && prim >= 0 && id < prim)) { dist = c; prim = id; result = 1; }
+    }
+    h.prim = prim;
+    h.result = result;
+    h.dist = dist;
+    unsigned tests = (unsigned)S.n, shadows = 0;
+    if (prim >= 0 && S.light[prim]) {                        // :197-200
+        const float4 c = S.col[prim];
+        h.col = mk(c.x, c.y, c.z);
+    } else if (prim >= 0) {
+        v3 pi;                                                // :203-205
+        pi.x = ray.o.x + (ray.d.x * dist);
+        pi.y = ray.o.y + (ray.d.y * dist);
+        pi.z = ray.o.z + (ray.d.z * dist);
+        h.pi = pi;
+        const float4 hc = S.col[prim];
+        const float4 hm = S.mat[prim];
+        const float pdiff = hm.z, pspec = hm.w;
+        const v3 N = normal_at(S, prim, pi);
+        for (int li = 0; li < S.nlights; li++) {              // :207-277, lights in index order
+            const int l = S.lights[li];
+            const float4 lc = S.cen[l];
+            const float4 lm = S.col[l];
+            float shade = 1.0f;
+            const v3 t = mk(lc.x - pi.x, lc.y - pi.y, lc.z - pi.z);
+            const float d2 = t.x * t.x + t.y * t.y + t.z * t.z;
+            float len, inv;
+            if (!wave_any(!sqrt_nr_ok(d2))) {                 // :218-223 L_LEN and 1.0f / L_LEN
+                len = sqrt_nr(d2);
+                inv = rcp_nr(len);
+            } else {
+                len = sqrt_rn(d2);
+                inv = 1.0f / len;
+            }
+            const v3 L = mk(inv * t.x, inv * t.y, inv * t.z);
+            if (S.type[l] == SPHERE) {                        // :224-241
+                ray3 r;
+                r.o = mk(pi.x + L.x * EPS, pi.y + L.y * EPS, pi.z + L.z * EPS);
+                r.d = L;
+                shadows++;
+                // Any non-light primitive nearer than the light centre shades
+                // the point; the reference stops at the first, so only its
+                // position matters (test counter).
+                int first = 0x7fffffff;
+                for (int k = 0; k < S.nos; k++) {
+                    int res;
+                    const float c = sphere_cand(S.osph[k], r, res);
+                    if (res && c < len) first = min(first, S.osph_pos[k]);
+                    if (!COUNT && !wave_any(first == 0x7fffffff)) break;
+                }
+#pragma unroll 4
+                for (int k = 0; k < S.nop; k++) {
+                    if (!COUNT && !wave_any(first == 0x7fffffff)) break;
+                    const float c = plane_cand(S.opln[k], r);
+                    if (c < len) first = min(first, S.opln_pos[k]);
+                }
+                if (first != 0x7fffffff) shade = 0.0f;
+                tests += first != 0x7fffffff ? (unsigned)first + 1u : (unsigned)S.nnonlight;
+            }
+            if (pdiff > 0) {                                  // :244-254
+                const float dp = N.x * L.x + N.y * L.y + N.z * L.z;
+                if (dp > 0) {
+                    const float diff = dp * pdiff * shade;
+                    h.col.x += diff * hc.x * lm.x;
+                    h.col.y += diff * hc.y * lm.y;
+                    h.col.z += diff * hc.z * lm.z;
+                }
+            }
+            // :256-275.  An occluded light adds (float)(pow * m_spec * 0.0) =
+            // +0 (pow of a dot <= ~1 is finite): only lit points evaluate pow.
+            if (pspec > 0 && shade > 0) {
+                const float td = L.x * N.x + L.y * N.y + L.z * N.z;
+                const v3 R = mk(L.x - 2.0f * td * N.x, L.y - 2.0f * td * N.y, L.z - 2.0f * td * N.z);
+                const float dp = ray.d.x * R.x + ray.d.y * R.y + ray.d.z * R.z;
+                if (dp > 0) {
+                    const float spec = (float)(rtm::pow_d((double)dp, 20.0) * (double)pspec * (double)shade);
+                    h.col.x += spec * lm.x;
+                    h.col.y += spec * lm.y;
+                    h.col.z += spec * lm.z;
+                }
+            }
+        }
+    }
+    h.cnt = COUNT ? (tests | (shadows << 16)) : 0u;
+    return h;
+}
+
+// The term the pixel's accumulator receives when `n` is popped (:351-368).
+__device__ __forceinline__ v3 term(const Scene &S, const Node &n, const Hit &h)
+{
+    v3 c;
+    c.x = h.col.x * n.w;
+    c.y = h.col.y * n.w;
+    c.z = h.col.z * n.w;
+    if (n.type == 1) {
+        const float4 oc = S.col[n.origin];
+        c.x = c.x * oc.x * n.tr.x;
+        c.y = c.y * oc.y * n.tr.y;
+        c.z = c.z * oc.z * n.tr.z;
+    } else if (n.type == 2) {
+        c.x = c.x * n.tr.x;
+        c.y = c.y * n.tr.y;
+        c.z = c.z * n.tr.z;
+    }
+    return c;
+}
+
+// Children of `n` at depth < 5 (:370-432): bit 0 reflected child, bit 1
+// refracted child (none after total internal reflection).  A ray that hit
+// nothing or hit a light has undefined children in the reference
+// (primitives[-1], uninitialised point_intersect): none here, flagged by
+// bit 2 when the reference would have read them.
+__device__ __forceinline__ int expand(const Scene &S, const Node &n, const Hit &h, Node &cl, Node &cr)
+{
+    if (h.prim < 0) return 4;
+    const int p = h.prim;
+    const float4 pc = S.col[p];
+    const float4 pm = S.mat[p];
+    if (S.light[p]) return (pc.w > 0.0f || pm.x > 0.0f) ? 4 : 0;
+    int f = 0;
+    const float refl = pc.w;
+    if (refl > 0.0f) {                                        // :373-394
+        const v3 N = normal_at(S, p, h.pi);
+        const float td = n.r.d.x * N.x + n.r.d.y * N.y + n.r.d.z * N.z;
+        const v3 R = mk(n.r.d.x - 2.0f * td * N.x, n.r.d.y - 2.0f * td * N.y, n.r.d.z - 2.0f * td * N.z);
+        cl.r.o = mk(h.pi.x + R.x * EPS, h.pi.y + R.y * EPS, h.pi.z + R.z * EPS);
+        cl.r.d = R;
+        cl.w = refl * n.w;
+        cl.tr = n.tr;
+        cl.origin = p;
+        cl.type = 1;
+        cl.rcode = n.rcode;
+        f |= 1;
+    }
+    const float refr = pm.x;
+    if (refr > 0.0f) {                                        // :396-431
+        const float m_rindex = pm.y;
+        const float rin = n.rcode ? S.mat[n.rcode - 1].y : 1.0f;
+        const float nn = rin / m_rindex;
+        const v3 t = normal_at(S, p, h.pi);
+        const float fr = (float)h.result;
+        const v3 N = mk(t.x * fr, t.y * fr, t.z * fr);
+        const float td = N.x * n.r.d.x + N.y * n.r.d.y + N.z * n.r.d.z;
+        const float cosI = -td;
+        const float cosT2 = 1.0f - nn * nn * (1.0f - cosI * cosI);
+        if (cosT2 > 0.0f) {
+            const float k = nn * cosI - sqrt_exact(cosT2);
+            const v3 T = mk((nn * n.r.d.x) + k * N.x, (nn * n.r.d.y) + k * N.y, (nn * n.r.d.z) + k * N.z);
+            cr.r.o = mk(h.pi.x + T.x * EPS, h.pi.y + T.y * EPS, h.pi.z + T.z * EPS);
+            cr.r.d = T;
+            cr.w = n.w;
+            const float nd = -h.dist;
+            cr.tr.x = n.tr.x * rtm::expf(pc.x * 0.15f * nd);
+            cr.tr.y = n.tr.y * rtm::expf(pc.y * 0.15f * nd);
+            cr.tr.z = n.tr.z * rtm::expf(pc.z * 0.15f * nd);
+            cr.origin = p;
+            cr.type = 2;
+            cr.rcode = p + 1;
+            f |= 2;
+        }
+    }
+    return f;
+}
+
+// Primary ray of sub-sample `sub` (tx outer, ty inner, :317-339) of the pixel
+// with SX = WX1 + x*DX, SY = WY1 + y*DY (:304-305).
+__device__ __forceinline__ Node primary(int sub, int x, int y, float DX, float DY)
+{
+    const float SX = -3.0f + x * DX, SY = 2.25f + y * DY;
+    const float tx = (float)(sub / 3 - 1), ty = (float)(sub % 3 - 1);
+    v3 d;
+    d.x = SX + DX * (tx / 2.0f) - 0.0f;
+    d.y = SY + DY * (ty / 2.0f) - 0.25f;
+    d.z = 0.0f - (-7.0f);
+    const float l = inv_len(d.x * d.x + d.y * d.y + d.z * d.z);
+    d.x *= l; d.y *= l; d.z *= l;
+    Node n;
+    n.r.o = mk(0.0f, 0.25f, -7.0f);
+    n.r.d = d;
+    n.w = 1.0f;
+    n.tr = mk(1.f, 1.f, 1.f);
+    n.origin = -1;
+    n.type = 0;
+    n.rcode = 0;
+    return n;
+}
+
+// Scene image from the reference's 96-byte Primitive_2 array (one block).
+__global__ void __launch_bounds__(64) scene_kernel(const rtq_primitive *__restrict__ prims, int nprims,
+                                                   Scene *__restrict__ out)
+{
+    Scene &S = *out;
+    for (int p = threadIdx.x; p < nprims; p += blockDim.x) {
+        const rtq_primitive &q = prims[p];
+        S.col[p] = make_float4(q.m_color.x, q.m_color.y, q.m_color.z, q.m_refl);
+        S.mat[p] = make_float4(q.m_refr, q.m_refr_index, q.m_diff, q.m_spec);
+        S.geo[p] = q.type == SPHERE ? make_float4(q.center.x, q.center.y, q.center.z, q.r_radius)
+                                    : make_float4(q.normal.x, q.normal.y, q.normal.z, 0.f);
+        S.cen[p] = make_float4(q.center.x, q.center.y, q.center.z, 0.f);
+        S.type[p] = q.type;
+        S.light[p] = q.is_light ? 1 : 0;
+    }
+    if (threadIdx.x == 0) {
+        int nl = 0, nn = 0, ns = 0, np = 0, nos = 0, nop = 0;
+        for (int p = 0; p < nprims; p++) {
+            const rtq_primitive &q = prims[p];
+            const bool occluder = !q.is_light;
+            if (q.is_light) S.lights[nl++] = p;
+            if (q.type == SPHERE) {
+                S.sph[ns] = make_float4(q.center.x, q.center.y, q.center.z, q.sq_radius);
+                S.sph_id[ns++] = p;
+                if (occluder) { S.osph[nos] = S.sph[ns - 1]; S.osph_pos[nos++] = nn; }
+            } else if (q.type == PLANE) {
+                S.pln[np] = make_float4(q.normal.x, q.normal.y, q.normal.z, q.depth);
+                S.pln_id[np++] = p;
+                if (occluder) { S.opln[nop] = S.pln[np - 1]; S.opln_pos[nop++] = nn; }
+            }
+            if (occluder) nn++;
+        }
+        S.n = nprims; S.nlights = nl; S.nnonlight = nn;
+        S.ns = ns; S.np = np; S.nos = nos; S.nop = nop;
+    }
+}
+
+__device__ __forceinline__ void load_scene(Scene &S, const Scene *__restrict__ g)
+{
+    static_assert(sizeof(Scene) % 16 == 0, "Scene image is copied in 16-B words");
+    const uint4 *src = (const uint4 *)g;
+    uint4 *dst = (uint4 *)&S;
+    for (int i = threadIdx.x; i < (int)(sizeof(Scene) / 16); i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Level pass.  count[] layout (zeroed per slab), one counter per 128-B line.
+constexpr int C_BASE = 0;                     // + L: pool base of level L (2..5; level 1 at 0)
+constexpr int C_SEG = C_BASE + LEVELS;        // + L * NSEG + s: length of segment s of level L (1..5)
+constexpr int C_TOTAL = C_SEG + LEVELS * lq::NSEG;
+#define QCNT(A, i) ((A).count[(i) * lq::CSTRIDE])
+
+// Node record info word: heap index | origin primitive << 8 | type << 16 | rcode << 20.
+__device__ __forceinline__ int pack_info(int node, const Node &n)
+{
+    return node | ((n.origin & 0xff) << 8) | (n.type << 16) | (n.rcode << 20);
+}
+
+// Work-counter word of a node: tests | shadow rays << 16 | undefined-behaviour bit << 24.
+constexpr unsigned CNT_UB = 1u << 24;
+
+struct QArgs {
+    const Scene *scene;
+    float4 *rcol;         // [ntrees] root term.xyz, counter word (bits)
+    int2 *rchild;         // [ntrees] pool slots of the root's children, -1 if none
+    float4 *psum;         // [npix] the pixel's leading childless trees summed (xyz), first recorded sub (w, bits)
+    unsigned *fixbits;    // [ntrees/32 + 1] tree re-evaluated by final_kernel
+    // The record pool (levels 1..5), indexed by pool slot.
+    float4 *ia;           // queued ray: o.xyz, d.x
+    float4 *ib;           // d.y, d.z, weight, tree (bits)
+    float4 *ic;           // transparency.xyz, info (bits, pack_info)
+    float4 *ncol;         // node term.xyz, counter word (bits)
+    int2 *nchild;         // pool slots of the node's children (levels 1..4)
+    int *count;           // [C_TOTAL * CSTRIDE]
+    int pool, ntrees, npix, w;
+    int row_begin, row_stride;   // the slab's rows: see slab_row
+};
+
+__device__ __forceinline__ int slab_row(const QArgs &A, int r)
+{
+    return A.row_begin + ((r >> 4) * A.row_stride << 4) + (r & 15);
+}
+
+__device__ __forceinline__ int level_base(const QArgs &A, int L)
+{
+    return L <= 1 ? 0 : QCNT(A, C_BASE + L);
+}
+
+__device__ __forceinline__ void flag_tree(const QArgs &A, int tree)
+{
+    atomicOr(&A.fixbits[tree >> 5], 1u << (tree & 31));
+}
+
+__device__ __forceinline__ bool flagged(const QArgs &A, int tree)
+{
+    return (A.fixbits[tree >> 5] >> (tree & 31)) & 1u;
+}
+
+__device__ __forceinline__ void put_item(const QArgs &A, int slot, const Node &n, int tree, int node)
+{
+    A.ia[slot] = make_float4(n.r.o.x, n.r.o.y, n.r.o.z, n.r.d.x);
+    A.ib[slot] = make_float4(n.r.d.y, n.r.d.z, n.w, __int_as_float(tree));
+    A.ic[slot] = make_float4(n.tr.x, n.tr.y, n.tr.z, __int_as_float(pack_info(node, n)));
+}
+
+// Queues the children (flags f) of node `node` of `tree` into level L+1 and
+// returns their slots (-1: none).  All lanes of the wave call it.
+__device__ __forceinline__ int2 queue_children(const QArgs &A, int L, int nbase, int wave_id, bool active, int f,
+                                               const Node &cl, const Node &cr, int tree, int node)
+{
+    const bool ql = active && (f & 1), qr = active && (f & 2);
+    const int seg = wave_id & (lq::NSEG - 1);
+    const int lim = lq::seg_limit(A.pool, nbase);
+    int j = lq::wave_alloc(&QCNT(A, C_SEG + (L + 1) * lq::NSEG + seg), (int)ql + (int)qr);
+    int2 ch = make_int2(-1, -1);
+    if (ql) {
+        if (j < lim) {
+            ch.x = lq::seg_slot(nbase, seg, j);
+            put_item(A, ch.x, cl, tree, 2 * node + 1);
+        } else {
+            flag_tree(A, tree);
+        }
+        j++;
+    }
+    if (qr) {
+        if (j < lim) {
+            ch.y = lq::seg_slot(nbase, seg, j);
+            put_item(A, ch.y, cr, tree, 2 * node + 2);
+        } else {
+            flag_tree(A, tree);
+        }
+    }
+    return ch;
+}
+
+#ifndef RT_Q_MINWAVES
+#define RT_Q_MINWAVES 6
+#endif
+
+// Level 0: the nine primary rays of every pixel of the slab.
+template <bool COUNT>
+__global__ void __launch_bounds__(256, RT_Q_MINWAVES)
+root_kernel(QArgs A, int row_end, float DX, float DY, unsigned long long *__restrict__ counters)
+{
+    __shared__ Scene S;
+    load_scene(S, A.scene);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int r = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int y = slab_row(A, r);
+    const bool active = x < A.w && y < row_end;
+    const int pix = r * A.w + x;
+    const int wave_id = ((blockIdx.y * gridDim.x + blockIdx.x) << 2) + wave;
+    unsigned long long cnt[4] = {0, 0, 0, 0};
+    // While the pixel's trees have no children their terms are final: they
+    // are summed here in the reference's order; the trees from the first one
+    // with children on are recorded for the later passes.
+    float ax = 0.f, ay = 0.f, az = 0.f;
+    int kfirst = NSUB;
+    for (int sub = 0; sub < NSUB; sub++) {
+        Node n, cl, cr;
+        Hit h;
+        int f = 0;
+        if (active) {
+            n = primary(sub, x, y, DX, DY);
+            h = trace<COUNT>(S, n.r);
+            f = expand(S, n, h, cl, cr);
+        }
+        const int tree = sub * A.npix + pix;
+        const int2 ch = queue_children(A, 0, 0, wave_id, active, f, cl, cr, tree, 0);
+        if (active) {
+            const v3 c = term(S, n, h);     // weight 1, type ORIGIN: ray_col * 1.0f
+            const unsigned cw = h.cnt | ((f & 4) ? CNT_UB : 0u);
+            if (kfirst == NSUB && !(f & 3)) {
+                ax += c.x; ay += c.y; az += c.z;
+                if (COUNT) {
+                    cnt[0] += 1; cnt[1] += (cw >> 16) & 0xff; cnt[2] += cw & 0xffff; cnt[3] += cw >> 24;
+                }
+            } else {
+                if (kfirst == NSUB) kfirst = sub;
+                A.rcol[tree] = make_float4(c.x, c.y, c.z, __uint_as_float(cw));
+                A.rchild[tree] = ch;
+            }
+        }
+    }
+    if (active) A.psum[pix] = make_float4(ax, ay, az, __int_as_float(kfirst));
+    if (COUNT) flush_counters<4>(counters, cnt);
+}
+
+// Level L = 1..5: a grid of resident blocks; wave w takes 64-ray pages
+// w, w + #waves, ... of the level's queue.
+template <bool COUNT>
+__global__ void __launch_bounds__(256, RT_Q_MINWAVES)
+level_kernel(QArgs A, int L)
+{
+    __shared__ Scene S;
+    load_scene(S, A.scene);
+    const int base0 = level_base(A, L);
+    const lq::SegView v = lq::seg_view(&QCNT(A, C_SEG + L * lq::NSEG), base0, lq::seg_limit(A.pool, base0));
+    const int nbase = lq::next_base(v);             // level L+1's pool base
+    if (L < LEVELS - 1 && blockIdx.x == 0 && threadIdx.x == 0) QCNT(A, C_BASE + L + 1) = nbase;
+    const int lane = __lane_id();
+    const int wave_id = (blockIdx.x << 2) + (threadIdx.x >> 6);
+    int base, nvalid;
+    for (int k = wave_id; lq::seg_chunk(v, k, base, nvalid); k += gridDim.x << 2) {
+        const int q = base + lane;
+        const bool active = lane < nvalid;
+        Node n, cl, cr;
+        Hit h;
+        int f = 0, tree = 0, node = 0;
+        if (active) {
+            const float4 a = A.ia[q], b = A.ib[q], c = A.ic[q];
+            const int info = __float_as_int(c.w);
+            node = info & 0xff;
+            n.r.o = mk(a.x, a.y, a.z);
+            n.r.d = mk(a.w, b.x, b.y);
+            n.w = b.z;
+            tree = __float_as_int(b.w);
+            n.tr = mk(c.x, c.y, c.z);
+            n.origin = (info >> 8) & 0xff;
+            n.type = (info >> 16) & 0xf;
+            n.rcode = info >> 20;
+            h = trace<COUNT>(S, n.r);
+            if (L < LEVELS - 1) f = expand(S, n, h, cl, cr);
+            const v3 t = term(S, n, h);
+            const unsigned cw = h.cnt | ((f & 4) ? CNT_UB : 0u);
+            A.ncol[q] = make_float4(t.x, t.y, t.z, __uint_as_float(cw));
+        }
+        if (L < LEVELS - 1) {
+            const int2 ch = queue_children(A, L, nbase, wave_id, active, f, cl, cr, tree, node);
+            if (active) A.nchild[q] = ch;
+        }
+    }
+}
+
+// Node `j` (heap index) of a tree re-derived from its root: the ancestors'
+// rays are re-traced (not counted), node j traced and its term returned.
+// false if node j does not exist.
+template <bool COUNT>
+__device__ bool derive_node(const Scene &S, const Node &root, int j, Node &n, Hit &h, int &f, Node &cl, Node &cr)
+{
+    const unsigned hp = (unsigned)j + 1u;
+    const int depth = 31 - __builtin_clz(hp);
+    n = root;
+    for (int k = depth - 1; k >= 0; k--) {
+        const Hit ha = trace<false>(S, n.r);
+        Node a, b;
+        const int fa = expand(S, n, ha, a, b);
+        const bool refr_side = (hp >> k) & 1u;
+        if (!(fa & (refr_side ? 2 : 1))) return false;
+        n = refr_side ? b : a;
+    }
+    h = trace<COUNT>(S, n.r);
+    f = depth < LEVELS - 1 ? expand(S, n, h, cl, cr) : 0;
+    return true;
+}
+
+// The pixel's sum in the reference's order and the uchar4 pack (:436-447).
+template <bool COUNT>
+__global__ void __launch_bounds__(256)
+final_kernel(QArgs A, int row_end, float DX, float DY, uint32_t *__restrict__ out,
+             unsigned long long *__restrict__ counters)
+{
+    __shared__ Scene S;
+    __shared__ int ring[RING][256];
+    load_scene(S, A.scene);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int r = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int y = slab_row(A, r);
+    unsigned long long cnt[4] = {0, 0, 0, 0};
+    const auto count = [&](unsigned cw) {
+        cnt[0] += 1; cnt[1] += (cw >> 16) & 0xff; cnt[2] += cw & 0xffff; cnt[3] += cw >> 24;
+    };
+    if (x < A.w && y < row_end) {
+        const int pix = r * A.w + x;
+        const float4 ps = A.psum[pix];
+        float ax = ps.x, ay = ps.y, az = ps.z;
+        for (int sub = __float_as_int(ps.w); sub < NSUB; sub++) {
+            const int tree = sub * A.npix + pix;
+            if (flagged(A, tree)) {
+                // A node did not fit the pool: every node of the tree, in
+                // heap order, re-derived from the root.
+                const Node root = primary(sub, x, y, DX, DY);
+                unsigned long long todo = 1ull;
+                while (todo) {
+                    const int j = __builtin_ctzll(todo);
+                    todo &= todo - 1ull;
+                    Node n, cl, cr;
+                    Hit h;
+                    int f;
+                    if (!derive_node<COUNT>(S, root, j, n, h, f, cl, cr)) continue;
+                    const v3 c = term(S, n, h);
+                    ax += c.x; ay += c.y; az += c.z;
+                    if (COUNT) count(h.cnt | ((f & 4) ? CNT_UB : 0u));
+                    if (f & 1) todo |= 1ull << (2 * j + 1);
+                    if (f & 2) todo |= 1ull << (2 * j + 2);
+                }
+                continue;
+            }
+            const float4 c0 = A.rcol[tree];
+            ax += c0.x; ay += c0.y; az += c0.z;
+            if (COUNT) count(__float_as_uint(c0.w));
+            // Breadth-first over the recorded children: ring entries are pool
+            // slots with the node's level in bits 29..31.
+            int head = 0, tail = 0;
+            const int2 ch = A.rchild[tree];
+            if (ch.x >= 0) ring[tail++ & (RING - 1)][threadIdx.x] = ch.x | (1 << 29);
+            if (ch.y >= 0) ring[tail++ & (RING - 1)][threadIdx.x] = ch.y | (1 << 29);
+            while (head != tail) {
+                const int e = ring[head++ & (RING - 1)][threadIdx.x];
+                const int q = e & ((1 << 29) - 1), lvl = (unsigned)e >> 29;
+                const float4 c = A.ncol[q];
+                ax += c.x; ay += c.y; az += c.z;
+                if (COUNT) count(__float_as_uint(c.w));
+                if (lvl < LEVELS - 1) {
+                    const int2 cc = A.nchild[q];
+                    if (cc.x >= 0) ring[tail++ & (RING - 1)][threadIdx.x] = cc.x | ((lvl + 1) << 29);
+                    if (cc.y >= 0) ring[tail++ & (RING - 1)][threadIdx.x] = cc.y | ((lvl + 1) << 29);
+                }
+            }
+        }
+        // :436-441: (int) as x86 converts (an overflowing or NaN sum packs 0)
+        int red = cvt_i32_x86(ax * 28.0f), green = cvt_i32_x86(ay * 28.0f), blue = cvt_i32_x86(az * 28.0f);
+        if (red > 255) red = 255;
+        if (green > 255) green = 255;
+        if (blue > 255) blue = 255;
+        out[(size_t)y * A.w + x] = (uint32_t)(red & 0xff) | ((uint32_t)(green & 0xff) << 8) |
+                                   ((uint32_t)(blue & 0xff) << 16);
+    }
+    if (COUNT) flush_counters<4>(counters, cnt);
+}
+
+}  // namespace queue
+}  // namespace rt
+
+// ------------------------------------------------------------------ host side
+#include <stdlib.h>
+#include <algorithm>
+#include "rt_runtime.h"
+
+namespace {
+
+constexpr int SLOT_Q = 8;       // rtrt scratch slot of the queue tracer's arena
+
+// Trees per slab (1080p: two slabs) and the record pool as a fraction of
+// them: the reference scene needs 0.70 (3.02 M nodes below the roots for
+// 4.32 M trees at 800 x 600); a tree with a node that does not fit is
+// re-evaluated by final_kernel, exactly, so a denser scene is slower, never
+// wrong.
+constexpr long long SLAB_TREES = 12000000;
+constexpr double POOL_FRAC = 0.9;
+
+int wait_frame(rtrt::DeviceState &st)
+{
+    hipError_t e = hipEventSynchronize(st.wf_done);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtq frame wait");
+    st.wf_pending = false;
+    return RT_OK;
+}
+
+int arena(rtrt::DeviceState &st, int w, int rows, rt::queue::QArgs *A)
+{
+    using namespace rt::queue;
+    const size_t T = (size_t)w * rows * NSUB;
+    if (T > (size_t)0x7fffffff / 2) return rtrt::fail(RT_ERR_INVALID, "rtq: frame too large");
+    size_t P = (size_t)(T * POOL_FRAC);
+    if (const char *e = getenv("RT_QUEUE_POOL_CAP")) {      // test hook: exercises the overflow path
+        const long long v = atoll(e);
+        if (v > 0 && (size_t)v < P) P = (size_t)v;
+    }
+    P = std::max<size_t>((P + rt::lq::PAGE_ROW - 1) / rt::lq::PAGE_ROW, 1) * rt::lq::PAGE_ROW;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t FB = (T + 31) / 32 * 4;
+    const size_t bytes = al(sizeof(Scene)) + al(T * 16) + al(T * 8) + al((size_t)w * rows * 16) + al(FB) +
+                         al(P * 16) * 4 + al(P * 8) + al(sizeof(int) * C_TOTAL * rt::lq::CSTRIDE);
+    if (st.cap[SLOT_Q] < bytes && st.wf_pending) {
+        int rc = wait_frame(st);
+        if (rc) return rc;
+    }
+    void *base = nullptr;
+    int rc = rtrt::scratch(st, SLOT_Q, bytes, &base);
+    if (rc) return rc;
+    char *p = (char *)base;
+    auto take = [&](size_t b) { char *q = p; p += al(b); return q; };
+    A->scene = (const Scene *)take(sizeof(Scene));
+    A->rcol = (float4 *)take(T * 16);
+    A->rchild = (int2 *)take(T * 8);
+    A->psum = (float4 *)take((size_t)w * rows * 16);
+    A->fixbits = (unsigned *)take(FB);
+    A->ia = (float4 *)take(P * 16);
+    A->ib = (float4 *)take(P * 16);
+    A->ic = (float4 *)take(P * 16);
+    A->ncol = (float4 *)take(P * 16);
+    A->nchild = (int2 *)take(P * 8);
+    A->count = (int *)take(sizeof(int) * C_TOTAL * rt::lq::CSTRIDE);
+    A->pool = (int)P;
+    A->w = w;
+    return RT_OK;
+}
+
+template <class K>
+int resident_blocks(K kernel)
+{
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 1024;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per < 1) per = 1;
+    return cus * per;
+}
+
+template <bool COUNT>
+int launch(const rt::queue::QArgs &A, int w, int rows, int row_end, float DX, float DY, unsigned long long *cnt,
+           hipStream_t s, uint32_t *d_px)
+{
+    using namespace rt::queue;
+    static const int level_blocks = resident_blocks(level_kernel<COUNT>);
+    const dim3 tiles((w + 15) / 16, (rows + 15) / 16), block(256);
+    hipLaunchKernelGGL(root_kernel<COUNT>, tiles, block, 0, s, A, row_end, DX, DY, cnt);
+    for (int L = 1; L < LEVELS; L++) hipLaunchKernelGGL(level_kernel<COUNT>, dim3(level_blocks), block, 0, s, A, L);
+    hipLaunchKernelGGL(final_kernel<COUNT>, tiles, block, 0, s, A, row_end, DX, DY, d_px, cnt);
+    return rtrt::check_launch("rtq kernels");
+}
+
+}  // namespace
+
+extern "C" int rtq_render_async(const rtq_primitive *d_prims, int nprims, uint32_t *d_pixels, int w, int h,
+                                int row_begin, int row_end, uint64_t *d_counters, void *stream)
+{
+    if (!d_prims || !d_pixels || nprims < 1 || nprims > rt::queue::MAXP || w < 1 || h < 1)
+        return rtrt::fail(RT_ERR_INVALID, "rtq_render_async: bad arguments");
+    if (row_begin < 0 || row_end > h || row_begin >= row_end)
+        return rtrt::fail(RT_ERR_INVALID, "rtq_render_async: rows must satisfy 0 <= row_begin < row_end <= h");
+    rtrt::DeviceState *st;
+    int rc = rtrt::state(&st);
+    if (rc) return rc;
+    std::lock_guard<std::recursive_mutex> lk(st->mu);
+    hipStream_t s = (hipStream_t)stream;
+    // The arena belongs to the device: order this frame after the previous
+    // level-pass frame (queue tracer or Whitted), whatever stream it ran on.
+    if (st->wf_pending) {
+        hipError_t e = hipStreamWaitEvent(s, st->wf_done, 0);
+        if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render_async wait");
+    }
+    const float DX = (3.0f - -3.0f) / w, DY = (-2.25f - 2.25f) / h;     // :299-300
+    const int rows = row_end - row_begin;
+    const int ngroups = (rows + 15) / 16;
+    long long nslab = ((long long)w * ngroups * 16 * rt::queue::NSUB + SLAB_TREES - 1) / SLAB_TREES;
+    if (const char *e = getenv("RT_QUEUE_SLABS")) nslab = std::max(1, atoi(e));   // test hook
+    nslab = std::min<long long>(std::max<long long>(nslab, 1), ngroups);
+    const int slab_rows = (int)((ngroups + nslab - 1) / nslab) * 16;
+    rt::queue::QArgs A;
+    if ((rc = arena(*st, w, slab_rows, &A))) return rc;
+    A.row_stride = (int)nslab;
+    unsigned long long *cnt = (unsigned long long *)d_counters;
+    hipLaunchKernelGGL(rt::queue::scene_kernel, dim3(1), dim3(64), 0, s, d_prims, nprims,
+                       (rt::queue::Scene *)A.scene);
+    for (int k = 0; k < (int)nslab; k++) {
+        const int srows = (int)((ngroups - k + nslab - 1) / nslab) * 16;
+        A.row_begin = row_begin + 16 * k;
+        A.npix = w * srows;
+        A.ntrees = A.npix * rt::queue::NSUB;
+        hipError_t e = hipMemsetAsync(A.count, 0, sizeof(int) * rt::queue::C_TOTAL * rt::lq::CSTRIDE, s);
+        if (e == hipSuccess) e = hipMemsetAsync(A.fixbits, 0, sizeof(unsigned) * (((size_t)A.ntrees + 31) / 32), s);
+        if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render_async memset");
+        rc = cnt ? launch<true>(A, w, srows, row_end, DX, DY, cnt, s, d_pixels)
+                 : launch<false>(A, w, srows, row_end, DX, DY, cnt, s, d_pixels);
+        if (rc) return rc;
+    }
+    hipError_t e = hipEventRecord(st->wf_done, s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render_async record");
+    st->wf_pending = true;
+    return RT_OK;
+}
+
+extern "C" int rtq_render(const rtq_primitive *prims, int nprims, uint32_t *pixels, int w, int h,
+                          uint64_t *counters)
+{
+    if (!prims || !pixels || nprims < 1 || nprims > rt::queue::MAXP || w < 1 || h < 1)
+        return rtrt::fail(RT_ERR_INVALID, "rtq_render: bad arguments");
+    rtrt::DeviceState *st;
+    int rc = rtrt::state(&st);
+    if (rc) return rc;
+    std::lock_guard<std::recursive_mutex> lk(st->mu);
+    // slots 0..2 may still feed a frame issued on another stream
+    if (st->wf_pending && (rc = wait_frame(*st))) return rc;
+    const size_t frame_bytes = sizeof(uint32_t) * (size_t)w * h;
+    void *d_prims, *d_px, *d_cnt;
+    if ((rc = rtrt::scratch(*st, 0, sizeof(rtq_primitive) * nprims, &d_prims))) return rc;
+    if ((rc = rtrt::scratch(*st, 1, frame_bytes, &d_px))) return rc;
+    if ((rc = rtrt::scratch(*st, 2, 4 * sizeof(uint64_t), &d_cnt))) return rc;
+    hipStream_t s = st->stream;
+    hipError_t e = hipMemcpyAsync(d_prims, prims, sizeof(rtq_primitive) * nprims, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && counters) e = hipMemsetAsync(d_cnt, 0, 4 * sizeof(uint64_t), s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render H2D");
+    rc = rtq_render_async((const rtq_primitive *)d_prims, nprims, (uint32_t *)d_px, w, h, 0, h,
+                          counters ? (uint64_t *)d_cnt : nullptr, s);
+    if (rc) return rc;
+    e = hipMemcpyAsync(pixels, d_px, frame_bytes, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && counters)
+        e = hipMemcpyAsync(counters, d_cnt, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render D2H");
+    return RT_OK;
+}

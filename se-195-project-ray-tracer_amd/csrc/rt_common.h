@@ -89,6 +89,16 @@ __device__ __forceinline__ float inv_len(float d)
     return 1.f / sqrt_rn(d);
 }
 
+// (int)f as the reference's x86-64 build converts it (cvttss2si): truncation,
+// and INT_MIN -- the "integer indefinite" value -- for NaN and for values
+// outside [-2^31, 2^31).  v_cvt_i32_f32 saturates instead (and maps NaN to
+// 0), which would turn an overflowing accumulator into 255 where the
+// reference packs (unsigned char)INT_MIN = 0.
+__device__ __forceinline__ int cvt_i32_x86(float f)
+{
+    return (f >= -2147483648.0f && f < 2147483648.0f) ? (int)f : (int)0x80000000u;
+}
+
 // Wave-level u64 sum (64 lanes) used for the optional work counters.
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 {

@@ -22,6 +22,7 @@
 #define RT_GLIBC_MATH_H
 
 #include <stdint.h>
+#include "rt_glibc_pow_tables.h"
 
 #if defined(__HIPCC__)
 #define RTM_HD __host__ __device__ __forceinline__
@@ -289,6 +290,89 @@ RTM_HD void sincosf(float x, float &sn, float &cs)
     sn = odd ? pc : ps;
     cs = odd ? ps : pc;
     if (abstop < 0x398) { sn = x; cs = 1.0f; }
+}
+
+// glibc 2.35 double pow (e_pow.c), as its FMA build (__pow_fma, selected on
+// every x86-64 host with FMA/AVX2) evaluates it: every fma_d below is one
+// vfmadd/vfmsub of that build, every other op a plain IEEE double op, in its
+// order.  Used by the Raytracer3.2.03 queue tracer, whose g++-compiled
+// `pow(float, 20)` is this function at (double)x, 20.0
+// (raytracer_non_OpenCL.c:270).  Covers x > 0 normal and y with
+// 0x3be <= top12(y) < 0x43e (|y| in [2^-65, 2^63)); checked against the host
+// libm over every float x in (0, 4] at y = 20 (tests/test_glibc_math.py,
+// tests/test_gpu_math.py).
+RTM_HD double pow_d(double x, double y)
+{
+    using namespace powtab;
+    // log_inline: log(x) = k*ln2 + log(c) + log1p(z/c - 1) as hi + tail.
+    const uint64_t ix = d2u(x);
+    const uint64_t tmp = ix - 0x3fe6955500000000ull;
+    const int i = (int)((tmp >> 45) & 127u);
+    const double kd = (double)(int)((int64_t)tmp >> 52);
+    const double z = u2d(ix - (tmp & 0xfff0000000000000ull));
+    const double invc = LOG[i].invc, logc = LOG[i].logc, logctail = LOG[i].logctail;
+    const double r = fma_d(z, invc, -1.0);
+    const double t1 = fma_d(kd, LN2HI, logc);
+    const double t2 = r + t1;
+    const double lo1 = fma_d(kd, LN2LO, logctail);
+    const double lo2 = (t1 - t2) + r;
+    const double ar = r * A[0];
+    const double ar2 = r * ar;
+    const double ar3 = r * ar2;
+    const double hi = t2 + ar2;
+    const double lo3 = fma_d(ar, r, -ar2);
+    const double lo4 = (t2 - hi) + ar2;
+    const double q1 = fma_d(fma_d(r, A[6], A[5]), ar2, fma_d(r, A[4], A[3]));
+    const double q2 = fma_d(ar2, q1, fma_d(r, A[2], A[1]));
+    const double lo = fma_d(ar3, q2, ((lo1 + lo2) + lo3) + lo4);
+    const double lhi = hi + lo;
+    const double ltail = (hi - lhi) + lo;
+    // y * log(x) as ehi + elo.
+    const double ehi = y * lhi;
+    const double elo = fma_d(y, ltail, fma_d(lhi, y, -ehi));
+    // exp_inline(ehi, elo, sign_bias = 0).
+    const uint32_t abstop = (uint32_t)(d2u(ehi) >> 52) & 0x7ffu;
+    bool special = false;
+    if (abstop - 0x3c9u > 0x3eu) {
+        if ((int)(abstop - 0x3c9u) < 0) return 1.0 + ehi;          // |ehi| < 2^-54
+        if (abstop > 0x408u) return (d2u(ehi) >> 63) ? 0.0 : __builtin_inf();   // __math_uflow / oflow
+        special = true;                                            // 512 <= |ehi| < 1024
+    }
+    double kk = fma_d(ehi, INVLN2N, SHIFT);
+    const uint64_t ki = d2u(kk);
+    kk = kk - SHIFT;
+    double er = fma_d(kk, NEGLN2HIN, ehi);
+    er = fma_d(kk, NEGLN2LON, er);
+    const uint32_t idx = 2u * (uint32_t)(ki & 127u);
+    uint64_t sbits = EXP[idx + 1] + (ki << 45);
+    er = elo + er;
+    const double p23 = fma_d(er, C[1], C[0]);
+    const double tr = er + u2d(EXP[idx]);
+    const double r2 = er * er;
+    const double p45 = fma_d(er, C[3], C[2]);
+    const double e1 = fma_d(p23, r2, tr);
+    const double etmp = fma_d(p45, r2 * r2, e1);
+    if (!special) {
+        const double scale = u2d(sbits);
+        return fma_d(etmp, scale, scale);
+    }
+    // specialcase of e_exp.c (the scale's exponent over- or underflowed).
+    if ((ki & 0x80000000u) == 0) {
+        sbits -= 1009ull << 52;
+        const double scale = u2d(sbits);
+        return fma_d(scale, etmp, scale) * 0x1p1009;
+    }
+    sbits += 1022ull << 52;
+    const double scale = u2d(sbits);
+    double yy = scale + etmp * scale;
+    if (__builtin_fabs(yy) < 1.0) {
+        const double one = yy < 0.0 ? -1.0 : 1.0;
+        const double lo_ = (scale - yy) + etmp * scale;
+        const double hi_ = yy + one;
+        yy = ((((one - hi_) + yy) + lo_) + hi_) - one;
+        if (yy == 0) yy = u2d(sbits & 0x8000000000000000ull);
+    }
+    return yy * 0x1p-1022;
 }
 
 }  // namespace rtm

@@ -11,7 +11,7 @@
 
 namespace rtrt {
 
-constexpr int NSCRATCH = 8;
+constexpr int NSCRATCH = 9;
 constexpr int SLOT_VIEW = 7;
 
 struct DeviceState {

@@ -28,6 +28,7 @@
 //     op-for-op restatement of glibc 2.35's FMA build).
 #include "rt_common.h"
 #include "rt_glibc_math.h"
+#include "rt_levelq.h"
 
 namespace rt {
 namespace whitted {
@@ -386,12 +387,16 @@ constexpr int LEVELS = 6;
 constexpr int INFO_TIR = 0x100;       // refr > 0 but no refraction ray (TIR)
 constexpr int INFO_REFR_OK = 0x200;   // the node wrote a refraction ray
 constexpr int NODE_SHIFT = 16;        // linfo bits 16..21: the node's index (0..62)
-constexpr int NSEG = 64;
-constexpr int PAGE = 64;              // slots per page (one segment's)
-constexpr int PAGE_ROW = NSEG * PAGE; // one page of every segment
-// count[] layout (zeroed per slab).  Every counter has its own 128-B line
-// (same-line atomics serialise in the L2's atomic unit).
-constexpr int CSTRIDE = 32;
+using lq::NSEG;
+using lq::PAGE;
+using lq::PAGE_ROW;
+using lq::CSTRIDE;
+using lq::SegView;
+using lq::seg_slot;
+using lq::wave_alloc;
+using lq::next_base;
+using lq::seg_chunk;
+// count[] layout (zeroed per slab), one counter per 128-B line (lq::CSTRIDE).
 constexpr int C_FIX = 0;                      // trees flagged for fixup
 constexpr int C_TIR = 1;                      // + L: TIR list length of level L (0..4)
 constexpr int C_BASE = C_TIR + LEVELS;        // + L: pool base of level L (2..5; level 1 at 0)
@@ -430,15 +435,10 @@ __device__ __forceinline__ int slab_row(const WfArgs &A, int r)
     return A.row_begin + ((r >> 4) * A.row_stride << 4) + (r & 15);
 }
 
-// Pool slot of item j of segment s of the level based at `base`, and the
-// per-segment item limit of that level (the pages left in the pool).
-__device__ __forceinline__ int seg_slot(int base, int s, int j)
-{
-    return base + ((j >> 6) * NSEG + s) * PAGE + (j & (PAGE - 1));
-}
+// Per-segment item limit of a level based at `base` (the pages left in the pool).
 __device__ __forceinline__ int seg_limit(const WfArgs &A, int base)
 {
-    return (A.pool - base) / PAGE_ROW * PAGE;
+    return lq::seg_limit(A.pool, base);
 }
 __device__ __forceinline__ int level_base(const WfArgs &A, int L)
 {
@@ -457,23 +457,6 @@ __device__ void flag_tree(const WfArgs &A, int tree)
 __device__ __forceinline__ bool flagged(const WfArgs &A, int tree)
 {
     return (A.fixbits[tree >> 5] >> (tree & 31)) & 1u;
-}
-
-// Wave-aggregated queue allocation: every active lane asks for `want` (0..2)
-// items; one atomic per wave.  Returns the lane's first item index.
-__device__ __forceinline__ int wave_alloc(int *counter, int want)
-{
-    const unsigned long long m1 = __builtin_amdgcn_ballot_w64((want & 1) != 0);
-    const unsigned long long m2 = __builtin_amdgcn_ballot_w64((want & 2) != 0);
-    const int lane = __lane_id();
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    const int pre = __popcll(m1 & lt) + 2 * __popcll(m2 & lt);
-    const int tot = __popcll(m1) + 2 * __popcll(m2);
-    const int first = __builtin_ctzll(__builtin_amdgcn_read_exec());
-    int base = 0;
-    if (lane == first && tot) base = atomicAdd(counter, tot);
-    base = __shfl(base, first, 64);
-    return base + pre;
 }
 
 __device__ __forceinline__ void put_item(const WfArgs &A, int L, int slot, const ray3 &r, float rin, int tree,
@@ -527,46 +510,11 @@ __device__ __forceinline__ int node_info(const Hit &hh, bool tir)
     return (hh.prim & 0xff) | (tir ? INFO_TIR : 0) | (hh.refr_ray_ok ? INFO_REFR_OK : 0);
 }
 
-// Consumer view of level L's segmented queue: lane s holds segment s's length
-// and the inclusive prefix of its 64-item page counts.  Whole waves only.
-struct SegView { int incl, n, base; };
-
+// Consumer view of level L's segmented queue (rt_levelq.h).
 __device__ __forceinline__ SegView seg_view(const WfArgs &A, int L)
 {
-    const int lane = __lane_id();
-    SegView v;
-    v.base = level_base(A, L);
-    v.n = min(CNT(A, C_SEG + L * NSEG + lane), seg_limit(A, v.base));
-    int x = (v.n + PAGE - 1) / PAGE;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
-    v.incl = x;
-    return v;
-}
-
-// The pool base after level L: past the last page of its fullest segment.
-__device__ __forceinline__ int next_base(const SegView &v)
-{
-    int p = (v.n + PAGE - 1) / PAGE;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) p = max(p, __shfl_xor(p, off, 64));
-    return v.base + p * PAGE_ROW;
-}
-
-// Page k (wave-uniform) of the queue: first slot and number of valid items;
-// false once k is past the last page.
-__device__ __forceinline__ bool seg_chunk(const SegView &v, int k, int &base, int &nvalid)
-{
-    if (k >= __shfl(v.incl, 63, 64)) return false;
-    const int s = __popcll(__builtin_amdgcn_ballot_w64(v.incl <= k));
-    const int incl = __shfl(v.incl, s, 64), n = __shfl(v.n, s, 64);
-    const int c = k - (incl - ((n + PAGE - 1) / PAGE));
-    base = seg_slot(v.base, s, c * PAGE);
-    nvalid = min(PAGE, n - c * PAGE);
-    return true;
+    const int base = level_base(A, L);
+    return lq::seg_view(&CNT(A, C_SEG + L * NSEG), base, seg_limit(A, base));
 }
 
 #ifndef RT_WH_MINWAVES
@@ -811,7 +759,7 @@ final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
         tr += c0.x; tg += c0.y; tb += c0.z;
     }
     const float scale = A.ocl ? 64.0f : 28.0f;            // 256/4 (openCLcode.cl:238) or 256/9 (:517)
-    int red = (int)(tr * scale), green = (int)(tg * scale), blue = (int)(tb * scale);
+    int red = cvt_i32_x86(tr * scale), green = cvt_i32_x86(tg * scale), blue = cvt_i32_x86(tb * scale);
     if (red > 255) red = 255;
     if (green > 255) green = 255;
     if (blue > 255) blue = 255;

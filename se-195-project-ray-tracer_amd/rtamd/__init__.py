@@ -10,17 +10,20 @@ what the tests, bench.py and __graft_entry__ drive.
                (smallptgpu-v1.6/smallptCPU.cpp:77-132) on the GPU, or
                tiled in row bands over several GPUs (devices=[...]);
                SmallptMulti: the device-resident multi-GPU frame (spt_multi_*)
+    Queue    : queue_render()  ~ raytracer_non_kernel
+               (Raytracer3.2.03/.../raytracer_non_OpenCL.c:285-449) on the GPU
 """
 import ctypes as C
 
 import numpy as np
 
 from . import ppm, scenes
-from ._lib import (Camera, Primitive, RTError, Sphere, Vec3, check, device_count, lib,
+from ._lib import (Camera, Float4, Primitive, QPrimitive, RTError, Sphere, Vec3, check, device_count, lib,
                    set_device, SPT_DIRECT_LIGHTING, SPT_PATH_TRACING)
 
-__all__ = ["Camera", "Primitive", "Sphere", "Vec3", "RTError", "scenes", "lib", "check",
-           "device_count", "set_device", "whitted_render", "SmallptFrame", "SmallptScene", "SmallptMulti",
+__all__ = ["Camera", "Primitive", "QPrimitive", "Float4", "Sphere", "Vec3", "RTError", "scenes", "lib", "check",
+           "device_count", "set_device", "whitted_render", "queue_render", "SmallptFrame", "SmallptScene",
+           "SmallptMulti",
            "SPT_PATH_TRACING", "SPT_DIRECT_LIGHTING"]
 
 
@@ -53,6 +56,19 @@ def whitted_render_ocl(w, h, prims=None, nprims=None, frame=None, counters=False
     cnt = (C.c_uint64 * 4)()
     check(lib().rtw_render_ocl(C.addressof(prims), nprims, frame.ctypes.data, w, h,
                                C.addressof(cnt) if counters else None))
+    return (frame, list(cnt)) if counters else frame
+
+
+def queue_render(w, h, prims=None, nprims=None, counters=False):
+    """raytracer_non_kernel on the GPU: the uchar4 (r, g, b, 0) frame as
+    uint8 [h, w, 4].  Returns frame, or (frame, [rays, shadow rays, intersect
+    calls, undefined-behaviour events]) if counters."""
+    if prims is None:
+        prims, nprims = scenes.queue_scene()
+    frame = np.zeros((h, w, 4), dtype=np.uint8)
+    cnt = (C.c_uint64 * 4)()
+    check(lib().rtq_render(C.addressof(prims), nprims, frame.ctypes.data, w, h,
+                           C.addressof(cnt) if counters else None))
     return (frame, list(cnt)) if counters else frame
 
 

@@ -20,7 +20,8 @@ EXPORTS = ("rt_last_error", "rt_device_count", "rt_set_device", "rt_release", "r
            "spt_scene_create", "spt_scene_destroy", "spt_scene_render_async", "spt_pack_pixels_async",
            "spt_multi_create", "spt_multi_destroy", "spt_multi_set_scene", "spt_multi_bands", "spt_multi_upload",
            "spt_multi_render_async", "spt_multi_gather_async", "spt_multi_sync", "spt_multi_download",
-           "spt_multi_read_frame", "spt_multi_counters", "spt_multi_band_buffers", "spt_render_multi")
+           "spt_multi_read_frame", "spt_multi_counters", "spt_multi_band_buffers", "spt_render_multi",
+           "rtq_render", "rtq_render_async")
 
 
 class RTError(RuntimeError):
@@ -52,7 +53,21 @@ class Camera(C.Structure):
     _fields_ = [("orig", Vec3), ("target", Vec3), ("dir", Vec3), ("x", Vec3), ("y", Vec3)]
 
 
+class Float4(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float), ("w", C.c_float)]
+
+
+class QPrimitive(C.Structure):
+    """Raytracer3.2.03 raytracer_non_OpenCL.c:67-81 Primitive_2 (96 bytes)."""
+    _fields_ = [("m_color", Float4), ("m_refl", C.c_float), ("m_diff", C.c_float), ("m_refr", C.c_float),
+                ("m_refr_index", C.c_float), ("m_spec", C.c_float), ("dummy_3", C.c_float),
+                ("type", C.c_int32), ("is_light", C.c_uint8), ("pad_", C.c_uint8 * 3),
+                ("normal", Float4), ("center", Float4), ("depth", C.c_float), ("radius", C.c_float),
+                ("sq_radius", C.c_float), ("r_radius", C.c_float)]
+
+
 assert C.sizeof(Primitive) == 96 and C.sizeof(Sphere) == 44 and C.sizeof(Camera) == 60
+assert C.sizeof(QPrimitive) == 96
 
 _lib = None
 
@@ -100,6 +115,9 @@ def lib():
         L.spt_multi_band_buffers.argtypes = [vp, i, ip, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp),
                                              C.POINTER(vp)]
         L.spt_render_multi.argtypes = [vp, u, vp, vp, vp, vp, i, i, i, i, i, u64p, vp, i]
+    if hasattr(L, "rtq_render"):
+        L.rtq_render.argtypes = [vp, i, vp, i, i, u64p]
+        L.rtq_render_async.argtypes = [vp, i, vp, i, i, i, i, u64p, vp]
     _lib = L
     return L
 

@@ -9,13 +9,15 @@ These are the reference's own host-side inputs (not part of the device path):
   * read_scene()     -- ReadScene .scn parser (displayfunc.cpp:120-180)
   * hypersphere()    -- scene_build_complex.pl generator (:3-60)
   * complex10k()     -- the 10k-sphere config (BASELINE configs[4])
+  * queue_scene()    -- Raytracer3.2.03 create_scene (scene.c:48-97, CHOOSE_SCENE 0)
+                        after raytracer.c:721-746's copy into Primitive_2
 All float arithmetic is float32, in the reference's order.
 """
 import math
 
 import numpy as np
 
-from ._lib import Camera, Primitive, Sphere, Vec3
+from ._lib import Camera, Float4, Primitive, QPrimitive, Sphere, Vec3
 
 f32 = np.float32
 SPHERE, PLANE = 1, 2
@@ -222,3 +224,52 @@ def seeds(width, height, seed=1):
     out = np.empty(2 * width * height, dtype=np.uint32)
     lib().spt_seed_fill(out.ctypes.data, out.size, seed)
     return out
+
+
+# Raytracer3.2.03 scene.c:61-92 (CHOOSE_SCENE 0): kind, material (r, g, b, refl,
+# refr, refr_index, diff, spec), is_light, normal / centre xyz, depth / radius.
+_QUEUE = [
+    ("P", (0.6, 0.6, 0.6, 0.0, 0.0, 0.0, 0.4, 1.8), False, (0.0, 0.75, 0.0), 4.4),
+    ("S", (0.08, 0.08, 0.08, 0.2, 1.0, 1.4, 0.0, 0.0), False, (3.4, -3.4, 23.0), 2.5),
+    ("S", (0.07, 0.17, 0.07, 0.1, 1.0, 1.2, 0.0, 0.0), False, (-0.7, -4.90, 27.0), 1.0),
+    ("S", (1.0, 1.0, 1.0, 0.8, 0.0, 0.0, 0.0, 0.0), False, (-3.4, -3.4, 29.0), 2.5),
+    ("S", (1.5, 0.7, 0.7, 0.1, 0.0, 0.0, 0.2, 0.2), False, (0.5, -4.1, 29.0), 1.5),
+    ("S", (0.7, 0.7, 1.7, 0.2, 0.0, 0.0, 0.2, 0.2), False, (-6.0, -4.1, 32.0), 1.5),
+    ("S", (0.07, 0.17, 0.07, 0.3, 1.0, 1.2, 0.2, 0.8), False, (-6.7, -4.90, 29.0), 1.0),
+    ("S", (0.08, 0.08, 0.08, 0.7, 1.0, 1.3, 0.8, 0.0), False, (6.4, -4.9, 18.0), 1.0),
+    ("P", (1.0, 0.6, 0.6, 0.0, 0.0, 0.0, 0.8, 1.5), False, (0.7, 0.0, 0.0), 5.4),
+    ("P", (0.7, 0.6, 1.0, 0.0, 0.0, 0.0, 0.8, 0.8), False, (-0.7, 0.0, 0.0), 5.4),
+    ("P", (1.0, 1.0, 1.0, 0.0, 0.0, 0.0, 1.2, 0.8), False, (0.0, -0.8, 0.0), 5.4),
+    ("P", (1.5, 1.5, 1.5, 0.0, 0.0, 0.0, 1.2, 0.8), False, (0.0, 0.0, -0.14), 5.4),
+    ("P", (0.1, 0.1, 0.1, 0.0, 0.0, 0.0, 1.0, 1.0), False, (0.0, 0.0, 0.72), 5.4),
+    ("S", (0.85, 0.85, 0.85, 0.0, 0.0, 0.0, 0.0, 1.8), True, (0.0, 6.5, 22.0), 0.35),
+    ("S", (0.85, 0.85, 0.85, 0.0, 0.0, 0.0, 0.0, 1.8), True, (-3.0, 6.5, 22.0), 0.35),
+    ("S", (0.85, 0.85, 0.85, 0.0, 0.0, 0.0, 0.0, 1.8), True, (3.0, 6.5, 22.0), 0.35),
+]
+
+
+def queue_scene():
+    """create_scene + the Primitive -> Primitive_2 copy: 17 primitives, the
+    last one memset's zero record (n_primitives = 17 with 16 created,
+    scene.c:55) -- a PLANE of normal 0 that no ray hits but every shadow ray
+    tests.  Fields the reference leaves uninitialised (a sphere's normal, a
+    plane's centre, dummy_3, colour w) are 0 here; no computation reads them."""
+    P = (QPrimitive * 64)()
+    for k, (kind, m, light, v, d) in enumerate(_QUEUE):
+        p = P[k]
+        r, g, b, refl, refr, ri, diff, spec = [f32(x) for x in m]
+        p.m_color = Float4(r, g, b, 0)
+        p.m_refl, p.m_refr, p.m_refr_index, p.m_diff, p.m_spec = refl, refr, ri, diff, spec
+        p.is_light = 1 if light else 0
+        if kind == "P":
+            p.type = 0
+            p.normal = Float4(f32(v[0]), f32(v[1]), f32(v[2]), 0)
+            p.depth = f32(d)
+        else:
+            rad = f32(d)
+            p.type = 1
+            p.center = Float4(f32(v[0]), f32(v[1]), f32(v[2]), 0)
+            p.radius = rad
+            p.sq_radius = f32(rad * rad)
+            p.r_radius = f32(f32(1.0) / rad)
+    return P, len(_QUEUE) + 1

@@ -35,7 +35,19 @@ def lib():
         subprocess.run(["make", "-s", "-C", HERE, "libgpu_math_check.so"], check=True)
     L = C.CDLL(path)
     L.gmc_run.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+    L.gmc_run_pow20.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
     return L
+
+
+def pow20_check(lo=0x00000001, hi=0x40800000):
+    """rtm::pow_d(x, 20.0) on the device vs the host glibc pow for every float
+    x with bits in [lo, hi] (default: (0, 4]); (count, mismatches, first bad)."""
+    L = lib()
+    bad, first = C.c_uint64(), C.c_uint32()
+    rc = L.gmc_run_pow20(lo, hi, C.byref(bad), C.byref(first))
+    if rc != 0:
+        raise RuntimeError("gmc_run_pow20 failed (%d)" % rc)
+    return hi - lo + 1, bad.value, hex(first.value)
 
 
 def math_check(domains=DOMAINS):

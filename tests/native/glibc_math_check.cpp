@@ -66,6 +66,19 @@ int main(int argc, char **argv)
         [](float x) { float a, b; rtm::sincosf(x, a, b); return a; }, [](float x) { return ::sinf(x); });
     run("sincosf_branchless_cos_neg", 0x80000000u, 0x80000000u + trig_hi,
         [](float x) { float a, b; rtm::sincosf(x, a, b); return b; }, [](float x) { return ::cosf(x); });
+    // pow((double)dot, 20.0): Raytracer3.2.03 raytracer_non_OpenCL.c:270 (g++'s
+    // promoting std::pow), every float dot in (0, 4] -- double results compared.
+    {
+        const uint32_t hi = quick ? 0x3c000000u : 0x40800000u;
+        unsigned long long bad = 0, first = ~0ull;
+#pragma omp parallel for schedule(static, 1 << 16) reduction(+ : bad) reduction(min : first)
+        for (uint64_t u = 1; u <= hi; u++) {
+            const double x = (double)rtm::u2f((uint32_t)u);
+            if (rtm::d2u(rtm::pow_d(x, 20.0)) != rtm::d2u(::pow(x, 20.0))) { bad++; if (u < first) first = u; }
+        }
+        printf("pow_d_y20 %llu %llu 0x%08llx\n", (unsigned long long)hi, bad, first == ~0ull ? 0ull : first);
+        fflush(stdout);
+    }
     // The exact smallpt domain: r1 = (2*PI) * (m * 2^-23), m < 2^23.
     {
         unsigned long long bad = 0;

@@ -97,3 +97,48 @@ extern "C" int gmc_run(int fn, uint32_t lo, uint32_t hi, uint64_t *mismatches, u
     *first_bad = first;
     return 0;
 }
+
+// pow((double)x, 20.0) -- rtm::pow_d (Raytracer3.2.03 raytracer_non_OpenCL.c:270)
+// on the device vs the host glibc, double results compared bit for bit, for
+// the float bit patterns [lo, hi].
+__global__ void pow20_kernel(uint32_t lo, uint32_t n, uint64_t *out)
+{
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        out[i] = rtm::d2u(rtm::pow_d((double)rtm::u2f(lo + i), 20.0));
+}
+
+extern "C" int gmc_run_pow20(uint32_t lo, uint32_t hi, uint64_t *mismatches, uint32_t *first_bad)
+{
+    const uint32_t CH = 1u << 25;
+    uint64_t *d = nullptr;
+    std::vector<uint64_t> h(CH);
+    if (hipMalloc(&d, sizeof(uint64_t) * CH) != hipSuccess) return -1;
+    uint64_t bad = 0;
+    uint32_t first = 0xffffffffu;
+    for (uint64_t base = lo; base <= hi; base += CH) {
+        const uint32_t n = (uint32_t)((hi - base + 1) < CH ? (hi - base + 1) : CH);
+        hipLaunchKernelGGL(pow20_kernel, dim3(4096), dim3(256), 0, 0, (uint32_t)base, n, d);
+        if (hipMemcpy(h.data(), d, sizeof(uint64_t) * n, hipMemcpyDeviceToHost) != hipSuccess) {
+            (void)hipFree(d);
+            return -2;
+        }
+        const int T = 16;
+        std::vector<uint64_t> tb(T, 0);
+        std::vector<uint32_t> tf(T, 0xffffffffu);
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; t++)
+            th.emplace_back([&, t]() {
+                for (uint32_t i = t; i < n; i += T) {
+                    const double r = ::pow((double)rtm::u2f((uint32_t)base + i), 20.0);
+                    if (rtm::d2u(r) != h[i]) { tb[t]++; if ((uint32_t)base + i < tf[t]) tf[t] = (uint32_t)base + i; }
+                }
+            });
+        for (auto &x : th) x.join();
+        for (int t = 0; t < T; t++) { bad += tb[t]; if (tf[t] < first) first = tf[t]; }
+        if (base + CH > hi) break;
+    }
+    (void)hipFree(d);
+    *mismatches = bad;
+    *first_bad = first;
+    return 0;
+}

@@ -33,7 +33,20 @@ class Camera(C.Structure):  # camera.h:29-34, 60 B
     _fields_ = [("orig", V3), ("target", V3), ("dir", V3), ("x", V3), ("y", V3)]
 
 
+class F4(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float), ("w", C.c_float)]
+
+
+class QPrimitive(C.Structure):  # Primitive_2, Raytracer3.2.03 raytracer_non_OpenCL.c:67-81, 96 B
+    _fields_ = [("m_color", F4), ("m_refl", C.c_float), ("m_diff", C.c_float), ("m_refr", C.c_float),
+                ("m_refr_index", C.c_float), ("m_spec", C.c_float), ("dummy_3", C.c_float),
+                ("type", C.c_int32), ("is_light", C.c_uint8), ("pad_", C.c_uint8 * 3),
+                ("normal", F4), ("center", F4), ("depth", C.c_float), ("radius", C.c_float),
+                ("sq_radius", C.c_float), ("r_radius", C.c_float)]
+
+
 assert C.sizeof(Primitive) == 96 and C.sizeof(Sphere) == 44 and C.sizeof(Camera) == 60
+assert C.sizeof(QPrimitive) == 96
 
 _u64p = C.POINTER(C.c_uint64)
 _lib = None
@@ -65,6 +78,9 @@ def lib():
                                  C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_int, C.c_int, C.c_int, _u64p, C.c_int]
         L.ors_hypersphere.argtypes = [C.POINTER(Sphere), C.c_int, C.c_double]
+        L.orq_scene_init.argtypes = [C.POINTER(QPrimitive), C.c_int]
+        L.orq_render.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 _u64p, C.c_int]
         L.or_fnv1a64.argtypes = [C.c_void_p, C.c_size_t]
         L.or_fnv1a64.restype = C.c_uint64
         _lib = L
@@ -146,7 +162,99 @@ def hypersphere(max_depth, cap):
     return buf, total
 
 
+# ---------------------------------------------------------------- queue tracer (3.2.03)
+def queue_scene():
+    prims = (QPrimitive * 64)()
+    n = lib().orq_scene_init(prims, 64)
+    return prims, n
+
+
+def queue_render(w, h, prims=None, n=None, row_begin=0, row_end=None, nthreads=1):
+    """raytracer_non_kernel restated; returns (uint8 pixels[h,w,4], counters[4])."""
+    if prims is None:
+        prims, n = queue_scene()
+    if row_end is None:
+        row_end = h
+    px = np.zeros((h, w, 4), dtype=np.uint8)
+    cnt = (C.c_uint64 * 4)()
+    lib().orq_render(C.addressof(prims), n, px.ctypes.data, w, h, row_begin, row_end, cnt, nthreads)
+    return px, list(cnt)
+
+
+def queue_random_scene(rng, nspheres=12, nlights=3, nplanes_extra=0):
+    """A closed room of six planes (so no ray misses: the reference's
+    primitives[-1] read never happens) with random spheres: glass, mirrors,
+    diffuse, some overlapping or around the camera; lights with refl = refr = 0
+    (a light hit never spawns children in a defined way).  Test input only."""
+    P = (QPrimitive * 64)()
+    k = 0
+
+    def mat(p, col, refl, refr, ri, diff, spec):
+        p.m_color = F4(*[float(np.float32(c)) for c in col], 0.0)
+        p.m_refl, p.m_refr, p.m_refr_index, p.m_diff, p.m_spec = refl, refr, ri, diff, spec
+
+    walls = [((0.0, 0.75, 0.0), 4.4), ((0.7, 0.0, 0.0), 5.4), ((-0.7, 0.0, 0.0), 5.4),
+             ((0.0, -0.8, 0.0), 5.4), ((0.0, 0.0, -0.14), 5.4), ((0.0, 0.0, 0.72), 5.4)]
+    for _ in range(nplanes_extra):
+        v = rng.normal(size=3)
+        walls.append((tuple(v / np.linalg.norm(v)), float(rng.uniform(3, 9))))
+    order = list(range(len(walls) + nspheres + nlights))
+    rng.shuffle(order)
+    items = [("w", i) for i in range(len(walls))] + [("s", i) for i in range(nspheres)] + \
+            [("l", i) for i in range(nlights)]
+    for j in order:
+        kind, i = items[j]
+        p = P[k]
+        if kind == "w":
+            (nx, ny, nz), d = walls[i]
+            p.type = 0
+            p.normal = F4(nx, ny, nz, 0.0)
+            p.depth = d
+            mat(p, rng.uniform(0.1, 1.6, 3), 0.0 if rng.random() < 0.7 else float(rng.uniform(0, 0.5)), 0.0, 0.0,
+                float(rng.uniform(0.2, 1.2)), float(rng.choice([0.0, 0.8, 1.5, 1.8])))
+        elif kind == "s":
+            r = float(np.float32(rng.uniform(0.3, 2.6)))
+            p.type = 1
+            if i == 0 and rng.random() < 0.3:        # a sphere around the camera (0, 0.25, -7)
+                r = float(np.float32(0.4))
+                c = (0.0, 0.25, -7.0 + float(rng.uniform(0.0, 0.1)))
+            else:                                    # inside the room: no ray leaves it
+                c = (float(rng.uniform(-7.2 + r, 7.2 - r)), float(rng.uniform(-5.5 + r, 6.3 - r)),
+                     float(rng.uniform(-7.0 + r, 38.0 - r)))
+            p.center = F4(c[0], c[1], c[2], 0.0)
+            p.radius, p.sq_radius, p.r_radius = r, float(np.float32(r) * np.float32(r)), float(np.float32(1) / np.float32(r))
+            glass = rng.random() < 0.5
+            mat(p, rng.uniform(0.05, 1.7, 3), float(rng.uniform(0.05, 0.9)), 1.0 if glass else 0.0,
+                float(rng.uniform(1.05, 1.6)) if glass else 0.0, float(rng.choice([0.0, 0.2, 0.8])),
+                float(rng.choice([0.0, 0.2, 0.8])))
+        else:
+            r = 0.35
+            p.type = 1
+            p.is_light = 1
+            p.center = F4(float(rng.uniform(-5, 5)), float(rng.uniform(4, 6.5)), float(rng.uniform(10, 30)), 0.0)
+            p.radius, p.sq_radius, p.r_radius = r, float(np.float32(r) * np.float32(r)), float(np.float32(1) / np.float32(r))
+            mat(p, [0.85] * 3, 0.0, 0.0, 0.0, 0.0, 1.8)
+        k += 1
+    return P, k
+
+
 # ---------------------------------------------------------------- _ref
+def ref_queue_lib():
+    """oracle/_ref/libref_queue.so (Raytracer3.2.03's own CPU path), or None."""
+    path = os.path.join(ORACLE_DIR, "_ref", "libref_queue.so")
+    if not os.path.exists(path):
+        return None
+    Q = C.CDLL(path)
+    Q.ref_q_scene.argtypes = [C.POINTER(QPrimitive), C.c_int]
+    Q.ref_q_render.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(QPrimitive), C.c_int]
+    Q.ref_q_write_bmp.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p]
+    return Q
+
+
+def ref_queue_render(Q, w, h, prims, n):
+    px = np.zeros((h, w, 4), dtype=np.uint8)
+    Q.ref_q_render(px.ctypes.data, w, h, prims, n)
+    return px
 def ref_libs():
     """(whitted_scene_lib, smallpt_lib) built from /root/reference, or None."""
     d = os.path.join(ORACLE_DIR, "_ref")
