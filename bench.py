@@ -44,7 +44,7 @@ FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: peak FP32 vector
 W, H, SPP = 1920, 1080, 64
 
 
-BENCH_KERNEL = "rt::smallpt::render_kernel<false, false, 0>"
+BENCH_KERNEL = "rt::smallpt::render_kernel<false, false, 0, false>"
 
 
 def pmc_digest(kernel):
@@ -224,6 +224,61 @@ def configs0_line(args, dev):
             "cpu_threads": {"ms_per_frame": round(dtn * 1e3, 1), "Mrays_per_s": round(rays / dtn / 1e6, 3),
                             "cores": threads, "kind": "port", "sample": "oracle/whitted_oracle.c, the full frame"},
             "gpu": {"ms_per_frame": round(ms, 4), "Mrays_per_s": round(rays / ms / 1e3, 2)}}
+
+
+def queue_line(args, dev):
+    """Side line: the Raytracer3.2.03 queue tracer:
+    raytracer_non_kernel's frame at the reference's own 800x600
+    (raytracer.h:18-19) and at 1920x1080, one frame per launch sequence, HIP
+    events; CPU baselines: the port on the host share and the reference's own
+    raytracer_non_OpenCL.c (oracle/_ref) on one thread, both on the 800x600
+    frame."""
+    import oracle_lib as O
+    prims, n = rtamd.scenes.queue_scene()
+    d_prims = torch.frombuffer(bytearray(bytes(prims)[:96 * n]), dtype=torch.uint8).to(dev)
+    L = rtamd.lib()
+    s = torch.cuda.current_stream(dev)
+    out = {"workload": "Raytracer3.2.03 queue tracer (raytracer_non_kernel), reference scene, 9 primary rays/px"}
+    for w, h in [(800, 600), (W, H)]:
+        frame = torch.zeros(w * h, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+        run = lambda c: rtamd.check(L.rtq_render_async(d_prims.data_ptr(), n, frame.data_ptr(), w, h, 0, h,  # noqa: E731
+                                                       c.data_ptr() if c is not None else None, s.cuda_stream))
+        run(cnt)
+        torch.cuda.synchronize(dev)
+        counts = cnt.tolist()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 10
+        e0.record(s)
+        for _ in range(reps):
+            run(None)
+        e1.record(s)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / reps
+        rays = counts[0] + counts[1]
+        out["%dx%d" % (w, h)] = {"ms_per_frame": round(ms, 4), "Mrays_per_s": round(rays / ms / 1e3, 2),
+                                 "rays_per_frame": rays, "intersect_calls": counts[2],
+                                 "device_bytes": int(L.rt_cached_bytes())}
+    if not args.no_cpu:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        P, m = O.queue_scene()
+        t0 = time.perf_counter()
+        _, c = O.queue_render(800, 600, P, m, nthreads=threads)
+        dt = time.perf_counter() - t0
+        rays = c[0] + c[1]
+        out["cpu_baseline"] = {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads,
+                               "kind": "port", "ms_per_frame": round(dt * 1e3, 1),
+                               "sample": "oracle/queue_oracle.c, the 800x600 frame"}
+        Q = O.ref_queue_lib()
+        if Q is not None:
+            t0 = time.perf_counter()
+            O.ref_queue_render(Q, 800, 600, P, m)
+            dt = time.perf_counter() - t0
+            out["reference_1thread"] = {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": 1,
+                                        "kind": "reference", "ms_per_frame": round(dt * 1e3, 1),
+                                        "sample": "oracle/_ref/libref_queue.so (the reference's own "
+                                                  "raytracer_non_OpenCL.c), the 800x600 frame, one thread"}
+    return out
 
 
 def c5_line(args, dev):
@@ -451,6 +506,7 @@ def main():
         if not args.no_whitted:
             out["whitted"] = whitted_line(args, dev)
             out["configs4"] = c5_line(args, dev)
+            out["queue3203"] = queue_line(args, dev)
             if not args.no_cpu:
                 out["configs0"] = configs0_line(args, dev)
         out["cpu_baseline"] = None if args.no_cpu else cpu_baseline(args)

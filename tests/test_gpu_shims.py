@@ -3,8 +3,10 @@
     openCLcode, AllocateBuffers, SetKernelArguments, Engine_InitRender,
     AllocateBuffers, SetKernelArguments, ExecuteKernel, ReadKernelBuffer);
   * shim_smallpt.cpp in place of smallptGPU.cpp (SetUpOpenCL -> SetUpHIP,
-    then the idle loop's UpdateRenderingGPU calls).
-Both must reproduce the CPU path exactly."""
+    then the idle loop's UpdateRenderingGPU calls);
+  * shim_queue.cpp in place of Raytracer3.2.03's raytracer_non_OpenCL.c
+    (raytracer.c's main() with the reference's own scene.c / bitmap.c).
+All must reproduce the CPU path exactly."""
 import os
 import subprocess
 
@@ -165,3 +167,25 @@ def test_smallpt_drop_in_main(oracle, tmp_path):
     rc, rp = np.zeros(3 * w * h, np.float32), np.zeros(w * h, np.uint32)
     oracle.smallpt_render(S, n, cam, rc, seeds0, rp, w, h, 0, 3, nthreads=8)
     assert (px == rp).all()
+
+
+@pytest.mark.parametrize("w,h", [(800, 600), (640, 480)])
+def test_queue_shim_writes_the_reference_bmp(oracle, tmp_path, w, h):
+    """Raytracer3.2.03's main() sequence (create_scene, Primitive_2 copy,
+    raytracer_non_kernel -> the GPU, write_bmp_file) with the reference's own
+    scene.c and bitmap.c: at 800 x 600 (raytracer.h:18-19) the file is the
+    reference's committed test.bmp, byte for byte."""
+    import hashlib
+    import json
+    import rtamd.bmp
+    _build()
+    out = tmp_path / "test.bmp"
+    r = subprocess.run([os.path.join(NATIVE, "queue_ref_app"), str(w), str(h), str(out)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    data = out.read_bytes()
+    if (w, h) == (800, 600):
+        ka = json.load(open(os.path.join(os.path.dirname(NATIVE), "golden", "known_answers.json")))
+        assert hashlib.sha256(data).hexdigest() == ka["queue3203"]["test_bmp"]["sha256"]
+    ref, _ = oracle.queue_render(w, h, nthreads=8)
+    assert data == rtamd.bmp.bmp_bytes(ref)
