@@ -27,9 +27,12 @@
 //     leading trees without children were already summed by root_kernel, the
 //     rest are walked breadth-first through their child links (a 32-slot
 //     per-lane ring in LDS holds pool slots, not rays);
-//   * a tree with a node that did not fit the pool is re-evaluated in
-//     final_kernel itself, node by node in heap order, each node's ray
-//     re-derived from the root (registers only, no per-lane ray queue);
+//   * glibc's double pow (the specular term) is replaced by x^20 in five
+//     double multiplies plus a rounding certificate (spec20); a tree with a
+//     term it cannot certify (~1 evaluation in 2^24), or with a node that did
+//     not fit the pool, is flagged, and fix_kernel re-evaluates its pixel:
+//     node by node in heap order, each node's ray re-derived from the root
+//     (registers only, no per-lane ray queue), traced with rtm::pow_d;
 //   * the <= 64 primitives are staged per block into LDS as per-type SoA;
 //   * the reference's libm: sqrt -> correctly rounded sqrtf, exp(float) ->
 //     glibc expf, pow(float, 20) -> glibc's double pow (g++'s promoting
@@ -87,7 +90,29 @@ struct Hit {
     int result;           // HIT 1 / INPRIM -1
     float dist;
     unsigned cnt;         // tests | shadow rays << 16 (work counters)
+    bool amb;             // a specular term needs the exact pow (spec20)
 };
+
+// The specular factor (float)(pow((double)dp, 20.0) * (double)pspec) of
+// :270 -- g++'s promoting std::pow, i.e. glibc's double pow -- without the
+// table-driven pow.  x^20 by repeated squaring in double is within 2^-50 of
+// x^20 (a float x squares exactly; four more roundings), and glibc's pow is
+// within 0.52 ulp of it, so the double product glibc's value gives lies
+// within 2^-49 of d = p * pspec.  If d * (1 - 2^-48) and d * (1 + 2^-48)
+// round to the same float, so does that product (rounding is monotonic):
+// that float is the reference's.  Otherwise (a float rounding boundary within
+// 2^-48 of d, about one evaluation in 2^24) `amb` is set and the caller
+// re-evaluates the node with rtm::pow_d (EXACT).
+template <bool EXACT>
+__device__ __forceinline__ float spec20(float dp, float pspec, bool &amb)
+{
+    if (EXACT) return (float)(rtm::pow_d((double)dp, 20.0) * (double)pspec);
+    const double x = (double)dp, x2 = x * x, x4 = x2 * x2, x8 = x4 * x4, x16 = x8 * x8;
+    const double d = (x16 * x4) * (double)pspec;
+    const float lo = (float)(d * (1.0 - 0x1p-48)), hi = (float)(d * (1.0 + 0x1p-48));
+    amb |= lo != hi;
+    return lo;
+}
 
 // Sphere half of intersect (:111-148): the candidate distance (INPRIM: i2,
 // HIT: i1) or +inf with res = 0.
@@ -132,11 +157,13 @@ __device__ __forceinline__ v3 normal_at(const Scene &S, int p, v3 pt)
     return mk(0.f, 0.f, 0.f);
 }
 
-// raytrace, :179-281.
-template <bool COUNT>
+// raytrace, :179-281.  EXACT: the specular factor by rtm::pow_d (else
+// spec20's certified shortcut, h.amb when it cannot certify).
+template <bool COUNT, bool EXACT = false>
 __device__ Hit trace(const Scene &S, const ray3 &ray)
 {
     Hit h;
+    h.amb = false;
     h.col = mk(0.f, 0.f, 0.f);
     h.pi = mk(0.f, 0.f, 0.f);
     h.result = 1;
@@ -228,7 +255,8 @@ __device__ Hit trace(const Scene &S, const ray3 &ray)
                 const v3 R = mk(L.x - 2.0f * td * N.x, L.y - 2.0f * td * N.y, L.z - 2.0f * td * N.z);
                 const float dp = ray.d.x * R.x + ray.d.y * R.y + ray.d.z * R.z;
                 if (dp > 0) {
-                    const float spec = (float)(rtm::pow_d((double)dp, 20.0) * (double)pspec * (double)shade);
+                    // shade = 1 here: the reference's * (double)shade is exact
+                    const float spec = spec20<EXACT>(dp, pspec, h.amb);
                     h.col.x += spec * lm.x;
                     h.col.y += spec * lm.y;
                     h.col.z += spec * lm.z;
@@ -388,7 +416,8 @@ __device__ __forceinline__ void load_scene(Scene &S, const Scene *__restrict__ g
 
 // ---------------------------------------------------------------------------
 // Level pass.  count[] layout (zeroed per slab), one counter per 128-B line.
-constexpr int C_BASE = 0;                     // + L: pool base of level L (2..5; level 1 at 0)
+constexpr int C_FIX = 0;                      // pixels listed for fix_kernel
+constexpr int C_BASE = 1;                     // + L: pool base of level L (2..5; level 1 at 0)
 constexpr int C_SEG = C_BASE + LEVELS;        // + L * NSEG + s: length of segment s of level L (1..5)
 constexpr int C_TOTAL = C_SEG + LEVELS * lq::NSEG;
 #define QCNT(A, i) ((A).count[(i) * lq::CSTRIDE])
@@ -407,7 +436,9 @@ struct QArgs {
     float4 *rcol;         // [ntrees] root term.xyz, counter word (bits)
     int2 *rchild;         // [ntrees] pool slots of the root's children, -1 if none
     float4 *psum;         // [npix] the pixel's leading childless trees summed (xyz), first recorded sub (w, bits)
-    unsigned *fixbits;    // [ntrees/32 + 1] tree re-evaluated by final_kernel
+    unsigned *fixbits;    // [ntrees/32 + 1] tree whose records are incomplete or inexact
+    unsigned *pixbits;    // [npix/32 + 1] pixel with such a tree: finished by fix_kernel
+    int *fixlist;         // [fixcap] those pixels (fix_kernel scans pixbits when more)
     // The record pool (levels 1..5), indexed by pool slot.
     float4 *ia;           // queued ray: o.xyz, d.x
     float4 *ib;           // d.y, d.z, weight, tree (bits)
@@ -415,7 +446,7 @@ struct QArgs {
     float4 *ncol;         // node term.xyz, counter word (bits)
     int2 *nchild;         // pool slots of the node's children (levels 1..4)
     int *count;           // [C_TOTAL * CSTRIDE]
-    int pool, ntrees, npix, w;
+    int pool, fixcap, ntrees, npix, w;
     int row_begin, row_stride;   // the slab's rows: see slab_row
 };
 
@@ -429,14 +460,28 @@ __device__ __forceinline__ int level_base(const QArgs &A, int L)
     return L <= 1 ? 0 : QCNT(A, C_BASE + L);
 }
 
-__device__ __forceinline__ void flag_tree(const QArgs &A, int tree)
+// A tree whose records cannot give the reference's terms -- a node that did
+// not fit the pool, or a specular term spec20 could not certify -- is
+// re-evaluated with its pixel by fix_kernel.
+__device__ void flag_tree(const QArgs &A, int tree)
 {
-    atomicOr(&A.fixbits[tree >> 5], 1u << (tree & 31));
+    const unsigned bit = 1u << (tree & 31);
+    if (atomicOr(&A.fixbits[tree >> 5], bit) & bit) return;
+    const int pix = tree % A.npix;
+    const unsigned pb = 1u << (pix & 31);
+    if (atomicOr(&A.pixbits[pix >> 5], pb) & pb) return;
+    const int k = atomicAdd(&QCNT(A, C_FIX), 1);
+    if (k < A.fixcap) A.fixlist[k] = pix;
 }
 
-__device__ __forceinline__ bool flagged(const QArgs &A, int tree)
+__device__ __forceinline__ bool tree_flagged(const QArgs &A, int tree)
 {
     return (A.fixbits[tree >> 5] >> (tree & 31)) & 1u;
+}
+
+__device__ __forceinline__ bool pix_flagged(const QArgs &A, int pix)
+{
+    return (A.pixbits[pix >> 5] >> (pix & 31)) & 1u;
 }
 
 __device__ __forceinline__ void put_item(const QArgs &A, int slot, const Node &n, int tree, int node)
@@ -497,7 +542,7 @@ root_kernel(QArgs A, int row_end, float DX, float DY, unsigned long long *__rest
     unsigned long long cnt[4] = {0, 0, 0, 0};
     // While the pixel's trees have no children their terms are final: they
     // are summed here in the reference's order; the trees from the first one
-    // with children on are recorded for the later passes.
+    // with children (or with an uncertified term) on are recorded.
     float ax = 0.f, ay = 0.f, az = 0.f;
     int kfirst = NSUB;
     for (int sub = 0; sub < NSUB; sub++) {
@@ -514,7 +559,7 @@ root_kernel(QArgs A, int row_end, float DX, float DY, unsigned long long *__rest
         if (active) {
             const v3 c = term(S, n, h);     // weight 1, type ORIGIN: ray_col * 1.0f
             const unsigned cw = h.cnt | ((f & 4) ? CNT_UB : 0u);
-            if (kfirst == NSUB && !(f & 3)) {
+            if (kfirst == NSUB && !(f & 3) && !h.amb) {
                 ax += c.x; ay += c.y; az += c.z;
                 if (COUNT) {
                     cnt[0] += 1; cnt[1] += (cw >> 16) & 0xff; cnt[2] += cw & 0xffff; cnt[3] += cw >> 24;
@@ -523,6 +568,7 @@ root_kernel(QArgs A, int row_end, float DX, float DY, unsigned long long *__rest
                 if (kfirst == NSUB) kfirst = sub;
                 A.rcol[tree] = make_float4(c.x, c.y, c.z, __uint_as_float(cw));
                 A.rchild[tree] = ch;
+                if (h.amb) flag_tree(A, tree);
             }
         }
     }
@@ -568,6 +614,7 @@ level_kernel(QArgs A, int L)
             const v3 t = term(S, n, h);
             const unsigned cw = h.cnt | ((f & 4) ? CNT_UB : 0u);
             A.ncol[q] = make_float4(t.x, t.y, t.z, __uint_as_float(cw));
+            if (h.amb) flag_tree(A, tree);
         }
         if (L < LEVELS - 1) {
             const int2 ch = queue_children(A, L, nbase, wave_id, active, f, cl, cr, tree, node);
@@ -576,9 +623,75 @@ level_kernel(QArgs A, int L)
     }
 }
 
+// Adds a recorded (unflagged) tree's terms to the pixel's chain, breadth-
+// first through the child links.  ring: this lane's RING-entry column (pool
+// slots with the node's level in bits 29..31).
+template <bool COUNT, int COLS>
+__device__ __forceinline__ void fold_tree(const QArgs &A, int tree, int (*ring)[COLS], float &ax, float &ay,
+                                          float &az, unsigned long long (&cnt)[4])
+{
+    const int t = threadIdx.x;
+    const float4 c0 = A.rcol[tree];
+    ax += c0.x; ay += c0.y; az += c0.z;
+    const auto count = [&](unsigned cw) {
+        cnt[0] += 1; cnt[1] += (cw >> 16) & 0xff; cnt[2] += cw & 0xffff; cnt[3] += cw >> 24;
+    };
+    if (COUNT) count(__float_as_uint(c0.w));
+    int head = 0, tail = 0;
+    const int2 ch = A.rchild[tree];
+    if (ch.x >= 0) ring[tail++ & (RING - 1)][t] = ch.x | (1 << 29);
+    if (ch.y >= 0) ring[tail++ & (RING - 1)][t] = ch.y | (1 << 29);
+    while (head != tail) {
+        const int e = ring[head++ & (RING - 1)][t];
+        const int q = e & ((1 << 29) - 1), lvl = (unsigned)e >> 29;
+        const float4 c = A.ncol[q];
+        ax += c.x; ay += c.y; az += c.z;
+        if (COUNT) count(__float_as_uint(c.w));
+        if (lvl < LEVELS - 1) {
+            const int2 cc = A.nchild[q];
+            if (cc.x >= 0) ring[tail++ & (RING - 1)][t] = cc.x | ((lvl + 1) << 29);
+            if (cc.y >= 0) ring[tail++ & (RING - 1)][t] = cc.y | ((lvl + 1) << 29);
+        }
+    }
+}
+
+// :436-447: (int) as x86 converts (an overflowing or NaN sum packs 0), 255
+// clamp, uchar_4 (r, g, b, 0).
+__device__ __forceinline__ uint32_t pack_pixel(float ax, float ay, float az)
+{
+    int red = cvt_i32_x86(ax * 28.0f), green = cvt_i32_x86(ay * 28.0f), blue = cvt_i32_x86(az * 28.0f);
+    if (red > 255) red = 255;
+    if (green > 255) green = 255;
+    if (blue > 255) blue = 255;
+    return (uint32_t)(red & 0xff) | ((uint32_t)(green & 0xff) << 8) | ((uint32_t)(blue & 0xff) << 16);
+}
+
+// The pixel's sum in the reference's order and the pack, for every pixel
+// whose trees' records are complete and exact (the others: fix_kernel).
+template <bool COUNT>
+__global__ void __launch_bounds__(256)
+final_kernel(QArgs A, int row_end, uint32_t *__restrict__ out, unsigned long long *__restrict__ counters)
+{
+    __shared__ int ring[RING][256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int r = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int y = slab_row(A, r);
+    unsigned long long cnt[4] = {0, 0, 0, 0};
+    const int pix = r * A.w + x;
+    if (x < A.w && y < row_end && !pix_flagged(A, pix)) {
+        const float4 ps = A.psum[pix];
+        float ax = ps.x, ay = ps.y, az = ps.z;
+        for (int sub = __float_as_int(ps.w); sub < NSUB; sub++)
+            fold_tree<COUNT, 256>(A, sub * A.npix + pix, ring, ax, ay, az, cnt);
+        out[(size_t)y * A.w + x] = pack_pixel(ax, ay, az);
+    }
+    if (COUNT) flush_counters<4>(counters, cnt);
+}
+
 // Node `j` (heap index) of a tree re-derived from its root: the ancestors'
-// rays are re-traced (not counted), node j traced and its term returned.
-// false if node j does not exist.
+// rays re-traced (uncounted; their spec terms do not shape the children),
+// node j traced exactly.  false if node j does not exist.
 template <bool COUNT>
 __device__ bool derive_node(const Scene &S, const Node &root, int j, Node &n, Hit &h, int &f, Node &cl, Node &cr)
 {
@@ -593,37 +706,42 @@ __device__ bool derive_node(const Scene &S, const Node &root, int j, Node &n, Hi
         if (!(fa & (refr_side ? 2 : 1))) return false;
         n = refr_side ? b : a;
     }
-    h = trace<COUNT>(S, n.r);
+    h = trace<COUNT, true>(S, n.r);
     f = depth < LEVELS - 1 ? expand(S, n, h, cl, cr) : 0;
     return true;
 }
 
-// The pixel's sum in the reference's order and the uchar4 pack (:436-447).
+// The pixels final_kernel skipped: the chain over all nine trees, recorded
+// trees from their records, flagged trees node by node in heap order, each
+// node's ray re-derived from the root and traced exactly.  Waves take listed
+// pixels (or, past the list's capacity, 32-pixel words of pixbits).
 template <bool COUNT>
-__global__ void __launch_bounds__(256)
-final_kernel(QArgs A, int row_end, float DX, float DY, uint32_t *__restrict__ out,
-             unsigned long long *__restrict__ counters)
+__global__ void __launch_bounds__(64)
+fix_kernel(QArgs A, float DX, float DY, uint32_t *__restrict__ out, unsigned long long *__restrict__ counters)
 {
+    const int nfix = QCNT(A, C_FIX);
+    if (nfix == 0) return;
     __shared__ Scene S;
-    __shared__ int ring[RING][256];
+    __shared__ int ring[RING][64];
     load_scene(S, A.scene);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int r = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const int y = slab_row(A, r);
+    const bool scan = nfix > A.fixcap;
+    const int nitems = scan ? (A.npix + 31) >> 5 : nfix;
     unsigned long long cnt[4] = {0, 0, 0, 0};
-    const auto count = [&](unsigned cw) {
-        cnt[0] += 1; cnt[1] += (cw >> 16) & 0xff; cnt[2] += cw & 0xffff; cnt[3] += cw >> 24;
-    };
-    if (x < A.w && y < row_end) {
-        const int pix = r * A.w + x;
-        const float4 ps = A.psum[pix];
-        float ax = ps.x, ay = ps.y, az = ps.z;
-        for (int sub = __float_as_int(ps.w); sub < NSUB; sub++) {
-            const int tree = sub * A.npix + pix;
-            if (flagged(A, tree)) {
-                // A node did not fit the pool: every node of the tree, in
-                // heap order, re-derived from the root.
+    for (int it = blockIdx.x * 64 + threadIdx.x; it < nitems; it += gridDim.x * 64) {
+        unsigned bits = scan ? A.pixbits[it] : 1u;
+        while (bits) {
+            const int bit = __builtin_ctz(bits);
+            bits &= bits - 1u;
+            const int pix = scan ? (it << 5) + bit : A.fixlist[it];
+            const int x = pix % A.w, y = slab_row(A, pix / A.w);
+            const float4 ps = A.psum[pix];
+            float ax = ps.x, ay = ps.y, az = ps.z;
+            for (int sub = __float_as_int(ps.w); sub < NSUB; sub++) {
+                const int tree = sub * A.npix + pix;
+                if (!tree_flagged(A, tree)) {
+                    fold_tree<COUNT, 64>(A, tree, ring, ax, ay, az, cnt);
+                    continue;
+                }
                 const Node root = primary(sub, x, y, DX, DY);
                 unsigned long long todo = 1ull;
                 while (todo) {
@@ -635,46 +753,22 @@ final_kernel(QArgs A, int row_end, float DX, float DY, uint32_t *__restrict__ ou
                     if (!derive_node<COUNT>(S, root, j, n, h, f, cl, cr)) continue;
                     const v3 c = term(S, n, h);
                     ax += c.x; ay += c.y; az += c.z;
-                    if (COUNT) count(h.cnt | ((f & 4) ? CNT_UB : 0u));
+                    if (COUNT) {
+                        const unsigned cw = h.cnt | ((f & 4) ? CNT_UB : 0u);
+                        cnt[0] += 1; cnt[1] += (cw >> 16) & 0xff; cnt[2] += cw & 0xffff; cnt[3] += cw >> 24;
+                    }
                     if (f & 1) todo |= 1ull << (2 * j + 1);
                     if (f & 2) todo |= 1ull << (2 * j + 2);
                 }
-                continue;
             }
-            const float4 c0 = A.rcol[tree];
-            ax += c0.x; ay += c0.y; az += c0.z;
-            if (COUNT) count(__float_as_uint(c0.w));
-            // Breadth-first over the recorded children: ring entries are pool
-            // slots with the node's level in bits 29..31.
-            int head = 0, tail = 0;
-            const int2 ch = A.rchild[tree];
-            if (ch.x >= 0) ring[tail++ & (RING - 1)][threadIdx.x] = ch.x | (1 << 29);
-            if (ch.y >= 0) ring[tail++ & (RING - 1)][threadIdx.x] = ch.y | (1 << 29);
-            while (head != tail) {
-                const int e = ring[head++ & (RING - 1)][threadIdx.x];
-                const int q = e & ((1 << 29) - 1), lvl = (unsigned)e >> 29;
-                const float4 c = A.ncol[q];
-                ax += c.x; ay += c.y; az += c.z;
-                if (COUNT) count(__float_as_uint(c.w));
-                if (lvl < LEVELS - 1) {
-                    const int2 cc = A.nchild[q];
-                    if (cc.x >= 0) ring[tail++ & (RING - 1)][threadIdx.x] = cc.x | ((lvl + 1) << 29);
-                    if (cc.y >= 0) ring[tail++ & (RING - 1)][threadIdx.x] = cc.y | ((lvl + 1) << 29);
-                }
-            }
+            out[(size_t)y * A.w + x] = pack_pixel(ax, ay, az);
         }
-        // :436-441: (int) as x86 converts (an overflowing or NaN sum packs 0)
-        int red = cvt_i32_x86(ax * 28.0f), green = cvt_i32_x86(ay * 28.0f), blue = cvt_i32_x86(az * 28.0f);
-        if (red > 255) red = 255;
-        if (green > 255) green = 255;
-        if (blue > 255) blue = 255;
-        out[(size_t)y * A.w + x] = (uint32_t)(red & 0xff) | ((uint32_t)(green & 0xff) << 8) |
-                                   ((uint32_t)(blue & 0xff) << 16);
     }
     if (COUNT) flush_counters<4>(counters, cnt);
 }
 
 }  // namespace queue
+
 }  // namespace rt
 
 // ------------------------------------------------------------------ host side
@@ -714,9 +808,11 @@ int arena(rtrt::DeviceState &st, int w, int rows, rt::queue::QArgs *A)
     }
     P = std::max<size_t>((P + rt::lq::PAGE_ROW - 1) / rt::lq::PAGE_ROW, 1) * rt::lq::PAGE_ROW;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t FB = (T + 31) / 32 * 4;
-    const size_t bytes = al(sizeof(Scene)) + al(T * 16) + al(T * 8) + al((size_t)w * rows * 16) + al(FB) +
-                         al(P * 16) * 4 + al(P * 8) + al(sizeof(int) * C_TOTAL * rt::lq::CSTRIDE);
+    const size_t npix = (size_t)w * rows;
+    const size_t FB = (T + 31) / 32 * 4, PB = (npix + 31) / 32 * 4;
+    const size_t FC = std::max<size_t>(npix / 64, 4096);       // listed pixels (fix_kernel)
+    const size_t bytes = al(sizeof(Scene)) + al(T * 16) + al(T * 8) + al(npix * 16) + al(FB) + al(PB) +
+                         al(FC * 4) + al(P * 16) * 4 + al(P * 8) + al(sizeof(int) * C_TOTAL * rt::lq::CSTRIDE);
     if (st.cap[SLOT_Q] < bytes && st.wf_pending) {
         int rc = wait_frame(st);
         if (rc) return rc;
@@ -731,6 +827,8 @@ int arena(rtrt::DeviceState &st, int w, int rows, rt::queue::QArgs *A)
     A->rchild = (int2 *)take(T * 8);
     A->psum = (float4 *)take((size_t)w * rows * 16);
     A->fixbits = (unsigned *)take(FB);
+    A->pixbits = (unsigned *)take(PB);
+    A->fixlist = (int *)take(FC * 4);
     A->ia = (float4 *)take(P * 16);
     A->ib = (float4 *)take(P * 16);
     A->ic = (float4 *)take(P * 16);
@@ -738,6 +836,7 @@ int arena(rtrt::DeviceState &st, int w, int rows, rt::queue::QArgs *A)
     A->nchild = (int2 *)take(P * 8);
     A->count = (int *)take(sizeof(int) * C_TOTAL * rt::lq::CSTRIDE);
     A->pool = (int)P;
+    A->fixcap = (int)FC;
     A->w = w;
     return RT_OK;
 }
@@ -761,7 +860,8 @@ int launch(const rt::queue::QArgs &A, int w, int rows, int row_end, float DX, fl
     const dim3 tiles((w + 15) / 16, (rows + 15) / 16), block(256);
     hipLaunchKernelGGL(root_kernel<COUNT>, tiles, block, 0, s, A, row_end, DX, DY, cnt);
     for (int L = 1; L < LEVELS; L++) hipLaunchKernelGGL(level_kernel<COUNT>, dim3(level_blocks), block, 0, s, A, L);
-    hipLaunchKernelGGL(final_kernel<COUNT>, tiles, block, 0, s, A, row_end, DX, DY, d_px, cnt);
+    hipLaunchKernelGGL(final_kernel<COUNT>, tiles, block, 0, s, A, row_end, d_px, cnt);
+    hipLaunchKernelGGL(fix_kernel<COUNT>, dim3(256), dim3(64), 0, s, A, DX, DY, d_px, cnt);
     return rtrt::check_launch("rtq kernels");
 }
 
@@ -805,6 +905,7 @@ extern "C" int rtq_render_async(const rtq_primitive *d_prims, int nprims, uint32
         A.ntrees = A.npix * rt::queue::NSUB;
         hipError_t e = hipMemsetAsync(A.count, 0, sizeof(int) * rt::queue::C_TOTAL * rt::lq::CSTRIDE, s);
         if (e == hipSuccess) e = hipMemsetAsync(A.fixbits, 0, sizeof(unsigned) * (((size_t)A.ntrees + 31) / 32), s);
+        if (e == hipSuccess) e = hipMemsetAsync(A.pixbits, 0, sizeof(unsigned) * (((size_t)A.npix + 31) / 32), s);
         if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render_async memset");
         rc = cnt ? launch<true>(A, w, srows, row_end, DX, DY, cnt, s, d_pixels)
                  : launch<false>(A, w, srows, row_end, DX, DY, cnt, s, d_pixels);
