@@ -83,6 +83,20 @@ def test_pool_overflow_reevaluates_exactly(rt, cap, monkeypatch):
     assert (px == r2).all() and cnt == c2
 
 
+def test_exact_path_everywhere(rt, monkeypatch):
+    """RT_QUEUE_EXACT_ALL=1: every specular term is treated as uncertified, so
+    nearly every pixel is finished by fix_kernel with glibc's pow restated
+    (rtm::pow_d) -- the same frame and counters."""
+    monkeypatch.setenv("RT_QUEUE_EXACT_ALL", "1")
+    px, cnt = rt.queue_render(800, 600, counters=True)
+    assert O.fnv1a64(px) == KA["800x600"]["frame_fnv"]
+    assert cnt == KA["800x600"]["counters"]
+    P, n = random_scene(5, 96, 72)
+    ref, rc = O.queue_render(96, 72, P, n, nthreads=NT)
+    px, cnt = rt.queue_render(96, 72, P, n, counters=True)
+    assert (px == ref).all() and cnt == rc
+
+
 @pytest.mark.parametrize("slabs", ["2", "5"])
 def test_slabs(rt, slabs, monkeypatch):
     monkeypatch.setenv("RT_QUEUE_SLABS", slabs)
