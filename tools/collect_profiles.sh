@@ -13,6 +13,6 @@ cp $S/pmc_digest.json $D/pmc_digest.json
 for d in $S/pmc*/; do
   n=$(basename $d)
   f=$(ls $d/*counter_collection.csv)
-  { head -1 $f; grep -E 'rt::(smallpt|whitted)::' $f || true; } > $D/${n}_render_kernels.csv
+  { head -1 $f; grep -E 'rt::(smallpt|whitted|queue)::' $f || true; } > $D/${n}_render_kernels.csv
 done
 ls -la $D

@@ -18,13 +18,13 @@ dur = defaultdict(list)
 for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        if "rt::smallpt::" not in name and "rt::whitted::" not in name:
+        if not any(t in name for t in ("rt::smallpt::", "rt::whitted::", "rt::queue::")):
             continue
         key = name.split("(")[0].replace("void ", "")
         acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for f in sorted(glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
-        if "rt::smallpt::" in r["Name"] or "rt::whitted::" in r["Name"]:
+        if any(t in r["Name"] for t in ("rt::smallpt::", "rt::whitted::", "rt::queue::")):
             dur[r["Name"].split("(")[0].replace("void ", "")].append(float(r["AverageNs"]))
 out = {}
 for k, c in acc.items():
