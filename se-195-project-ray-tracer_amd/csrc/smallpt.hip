@@ -370,6 +370,9 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
     while (true) {
         if (node < B.nnodes && pend == 0) {
             BVH_ST(0, 1);
+            BVH_ST(21, node < 64);
+            BVH_ST(22, node < 256);
+            BVH_ST(23, node < 1024);
             BVH_ST_WAVE(3);
             const float4 a = B.node[lay + 2u * (unsigned)node], b = B.node[lay + 2u * (unsigned)node + 1u];
             const int link = __float_as_int(a.w);
@@ -495,7 +498,7 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
         st[17] = vfar; st[18] = vfar ? st[0] : 0; st[19] = vfar && st[0] >= 512; st[20] = st[15] && st[0] >= 512;
     }
 #pragma unroll
-    for (int k = 0; k < 21; k++)
+    for (int k = 0; k < 24; k++)
         if (st[k]) atomicAdd(&g_bvh_stats[k], (unsigned long long)st[k]);   // divergent: per-lane atomics
 #endif
     return node >= B.nnodes && pend == 0;

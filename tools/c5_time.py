@@ -50,6 +50,8 @@ if stats:
               bs[7], bs[8], bs[9], bs[5], bs[11], bs[10] / max(bs[11], 1), bs[14], bs[12], bs[13] / max(bs[12], 1)))
     print("  alpha > 1/128: %d queries, %.1f nodes each, %d >= 512; origin > 8 root radii away: %d queries, "
           "%.1f nodes each, %d >= 512" % (bs[15], bs[16] / max(bs[15], 1), bs[20], bs[17], bs[18] / max(bs[17], 1), bs[19]))
+    print("  node visits in the first 64 / 256 / 1024 nodes of the ray's octant layout: %.3f %.3f %.3f" % (
+        bs[21] / max(bs[0], 1), bs[22] / max(bs[0], 1), bs[23] / max(bs[0], 1)))
 ts = []
 for _ in range(int(os.environ.get("REPS", "1"))):
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
