@@ -8,10 +8,12 @@ glibc rand() seeds) -- RadiancePathTracing for every sample of every pixel,
 running average, toInt pack -- plus, for N > 1, the RCCL all-gather that
 assembles the HDR accumulator and the RGBA8 frame on every rank.
 
-Rows are sharded over ranks in equal contiguous bands (strong scaling: the
-frame is fixed, each of N GPUs renders 1/N of it); for N > 1 one in-place
-RCCL all-gather of the HDR accumulator per frame, then every rank repacks the
-RGBA8 frame from it (spt_pack_pixels_async).  Frames are pipelined: frame
+Rows are sharded over ranks in interleaved 8-row groups (rank k renders groups
+k, k+N, ...: every GPU gets the same mix of the image; strong scaling: the
+frame is fixed, each of N GPUs renders 1/N of it; RT_BENCH_BANDS=1: equal
+contiguous bands instead); for N > 1 one RCCL all-gather of the HDR
+accumulator per frame, then every rank repacks the RGBA8 frame from it
+(spt_pack_pixels_async).  Frames are pipelined: frame
 i+1 renders while frame i is gathered (double-buffered frame, second stream).
 After the timed steps, rank 0's assembled frame is checked bit for bit
 against one GPU rendering the whole frame ("frame_check").  Rays = Intersect +
@@ -365,8 +367,9 @@ def main():
     seeds0 = torch.from_numpy(rtamd.scenes.seeds(W, H).view(np.int32)).to(dev)  # pristine
     seeds = torch.empty_like(seeds0)
     cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+    interleaved = world > 1 and not os.environ.get("RT_BENCH_BANDS")
     r0, r1 = rdist.row_band(rank, world, H)
-    B = r1 - r0
+    B = len(rdist.group_rows(rank, world, H)) if interleaved else r1 - r0
     s = torch.cuda.current_stream(dev)
     # N > 1 over RCCL: frames are pipelined -- frame i+1 renders (stream s)
     # while frame i's HDR all-gather and RGBA8 repack run on a second stream,
@@ -386,7 +389,8 @@ def main():
                                                 torch.cuda.current_stream(dev).cuda_stream))
         return pack
 
-    gathers = [rdist.FrameGather(colors[b], pixels[b], rank, world, W, H, pack=packer(b)) for b in range(nbuf)]
+    Gather = rdist.GroupGather if interleaved else rdist.FrameGather
+    gathers = [Gather(colors[b], pixels[b], rank, world, W, H, pack=packer(b)) for b in range(nbuf)]
     freed = [None] * nbuf        # event: buffer b's last gather finished
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
@@ -399,11 +403,16 @@ def main():
             s.wait_event(freed[b])
         if i is not None:
             ev[i][0].record(s)
-        rtamd.check(L.spt_scene_render_async(scene.handle, C.byref(cam), colors[b].data_ptr(),
-                                             seeds0.data_ptr(), seeds.data_ptr(), pixels[b].data_ptr(), W, H,
-                                             r0, r1, 0, SPP, rtamd.SPT_PATH_TRACING,
-                                             counters.data_ptr() if counters is not None else None,
-                                             s.cuda_stream))
+        cptr = counters.data_ptr() if counters is not None else None
+        if interleaved:
+            rtamd.check(L.spt_scene_render_groups_async(scene.handle, C.byref(cam), colors[b].data_ptr(),
+                                                        seeds0.data_ptr(), seeds.data_ptr(), pixels[b].data_ptr(),
+                                                        W, H, rank, world, 0, SPP, rtamd.SPT_PATH_TRACING, cptr,
+                                                        s.cuda_stream))
+        else:
+            rtamd.check(L.spt_scene_render_async(scene.handle, C.byref(cam), colors[b].data_ptr(),
+                                                 seeds0.data_ptr(), seeds.data_ptr(), pixels[b].data_ptr(), W, H,
+                                                 r0, r1, 0, SPP, rtamd.SPT_PATH_TRACING, cptr, s.cuda_stream))
         if i is not None:
             ev[i][1].record(s)
         if world > 1:            # RCCL all-gather of the HDR bands + RGBA8 repack
@@ -465,8 +474,9 @@ def main():
         "data": "synthetic: reference Cornell scene (scene.h:29-40), glibc rand() seeds, random-free camera",
         "config": {"workload": "smallpt Cornell 1920x1080 64spp RadiancePathTracing, one frame per step",
                    "frame": [W, H], "spp": SPP, "spheres": ns, "rows_per_gpu": B,
-                   "parallelism": ("row bands x%d + RCCL HDR all-gather%s" % (world, " (pipelined)" if pipelined else ""))
-                   if world > 1 else "single GPU"},
+                   "parallelism": ("%s x%d + RCCL HDR all-gather%s" % (
+                       "interleaved 8-row groups" if interleaved else "row bands", world,
+                       " (pipelined)" if pipelined else "")) if world > 1 else "single GPU"},
         "frames_per_s": round(1e3 / ms_per_step, 3),
         "Msamples_per_s": round(W * H * SPP / (ms_per_step * 1e-3) / 1e6, 2),
         "rays_per_frame": rays_per_frame,

@@ -163,6 +163,17 @@ int spt_scene_render_async(const spt_scene *scene, const rt_camera *camera, floa
                            int w, int h, int row_begin, int row_end, int first_sample, int nsamples,
                            int mode, uint64_t *d_counters, void *stream);
 
+/* spt_scene_render_async over an interleaved window: every pixel row y with
+ * (y / 8) % ngroups == group, i.e. 8-row groups group, group + ngroups, ...
+ * (0 <= group < ngroups).  The ngroups windows of a frame partition it; a
+ * multi-GPU frame split this way gives each GPU the same mix of the image
+ * (contiguous bands differ in cost with their content).  Same results per
+ * pixel as any other window. */
+int spt_scene_render_groups_async(const spt_scene *scene, const rt_camera *camera, float *d_colors,
+                                  const uint32_t *d_seeds_in, uint32_t *d_seeds_out, uint32_t *d_pixels,
+                                  int w, int h, int group, int ngroups, int first_sample, int nsamples,
+                                  int mode, uint64_t *d_counters, void *stream);
+
 /* The toInt pack of UpdateRenderingCPU (smallptCPU.cpp:120-122, vec.h:62)
  * alone: d_pixels[y*w+x] for rows [row_begin,row_end) from the accumulator
  * slots (h-y-1)*w+x of d_colors -- the pixels a render call writes, rebuilt

@@ -570,7 +570,7 @@ __global__ void __launch_bounds__(1024, GEO == 2 ? (COUNT ? RT_BVH_MINWAVES_COUN
 render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,
               uint32_t *seeds_out, uint32_t *__restrict__ pixels, int w, int h,
-              int row_begin, int row_end, int tiles_x, int ntiles, int first_sample, int nsamples,
+              int row_begin, int row_end, int tiles_x, int ntiles, int gstride, int first_sample, int nsamples,
               const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
               const float4 *__restrict__ g_col, const float4 *__restrict__ g_lrec, int nlights,
               BvhView bvh, unsigned long long *__restrict__ counters)
@@ -604,7 +604,9 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int tile = ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) * 4 + (wave & 3);
     const int x = (tile % tiles_x) * 8 + (lane & 7);
-    const int y = row_begin + (tile / tiles_x) * 8 + (lane >> 3);
+    // gstride > 1: the window is every gstride-th 8-row group from row_begin
+    // (spt_scene_render_groups_async, multi-GPU load balance).
+    const int y = row_begin + (tile / tiles_x) * 8 * gstride + (lane >> 3);
     const bool active = tile < ntiles && x < w && y < row_end;
 
     Counts cnt = {0, 0, 0, 0};
@@ -1067,12 +1069,16 @@ namespace {
 // four tiles per SIMD (a multi-GPU row band): then 1024-thread blocks with
 // more than half the CU's LDS reserved, so a CU holds exactly one and every
 // SIMD gets four waves, instead of the dispatcher's uneven 3..5 per SIMD.
-struct Shape { int tiles_x, ntiles, wpb, nblocks; };
-Shape launch_shape(const spt_scene &sc, int w, int r0, int r1)
+struct Shape { int tiles_x, ntiles, gstride, wpb, nblocks; };
+// Rows [r0, r1), or (gstride > 1) the 8-row groups r0/8, r0/8 + gstride, ...
+// below r1 (r0 a multiple of 8).
+Shape launch_shape(const spt_scene &sc, int w, int r0, int r1, int gstride = 1)
 {
     Shape g;
     g.tiles_x = (w + 7) / 8;
-    g.ntiles = g.tiles_x * ((r1 - r0 + 7) / 8);
+    g.gstride = gstride;
+    const int groups = (r1 - r0 + 7) / 8;
+    g.ntiles = g.tiles_x * ((groups + gstride - 1) / gstride);
     g.wpb = g.ntiles <= 16 * sc.cus ? 16 : 4;
     if (const char *e = getenv("RT_SPT_WPB")) g.wpb = atoi(e) == 16 ? 16 : 4;   // A/B
     g.nblocks = (g.ntiles + g.wpb - 1) / g.wpb;
@@ -1090,7 +1096,7 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     size_t lds = LDS ? (size_t)(3 * n + 3 * sc.nlights) * sizeof(float4) : 0;
     if (g.wpb == 16 && lds < 81 * 1024) lds = 81 * 1024;   // > half the CU's 160 KiB: one block per CU
     hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
-                       sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, first,
+                       sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.gstride, first,
                        ns, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt);
 }
 
@@ -1406,17 +1412,13 @@ extern "C" int spt_scene_destroy(spt_scene *sc)
     return RT_OK;
 }
 
-extern "C" int spt_scene_render_async(const spt_scene *sc, const rt_camera *camera, float *d_colors,
-                                      const uint32_t *d_seeds_in, uint32_t *d_seeds_out, uint32_t *d_pixels,
-                                      int w, int h, int row_begin, int row_end, int first_sample,
-                                      int nsamples, int mode, uint64_t *d_counters, void *stream)
+namespace {
+int scene_render(const spt_scene *sc, const rt_camera *camera, float *d_colors, const uint32_t *d_seeds_in,
+                 uint32_t *d_seeds_out, uint32_t *d_pixels, int w, int h, int row_begin, int row_end, int gstride,
+                 int first_sample, int nsamples, int mode, uint64_t *d_counters, void *stream)
 {
-    if (!sc) return rtrt::fail(RT_ERR_INVALID, "spt_scene_render_async: null scene");
-    int rc = check_render_args(camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, row_begin,
-                               row_end, first_sample, nsamples, mode);
-    if (rc) return rc;
-    if (row_begin == row_end) return RT_OK;
-    const Shape grid = launch_shape(*sc, w, row_begin, row_end);
+    if (row_begin >= row_end) return RT_OK;
+    const Shape grid = launch_shape(*sc, w, row_begin, row_end, gstride);
     hipStream_t s = (hipStream_t)stream;
     unsigned long long *cnt = (unsigned long long *)d_counters;
     const bool dl = mode == SPT_DIRECT_LIGHTING;
@@ -1432,6 +1434,35 @@ extern "C" int spt_scene_render_async(const spt_scene *sc, const rt_camera *came
         launch_mode<rt::smallpt::GEO_GLOBAL>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
                               d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
     return rtrt::check_launch("spt render_kernel");
+}
+}  // namespace
+
+extern "C" int spt_scene_render_async(const spt_scene *sc, const rt_camera *camera, float *d_colors,
+                                      const uint32_t *d_seeds_in, uint32_t *d_seeds_out, uint32_t *d_pixels,
+                                      int w, int h, int row_begin, int row_end, int first_sample,
+                                      int nsamples, int mode, uint64_t *d_counters, void *stream)
+{
+    if (!sc) return rtrt::fail(RT_ERR_INVALID, "spt_scene_render_async: null scene");
+    int rc = check_render_args(camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, row_begin,
+                               row_end, first_sample, nsamples, mode);
+    if (rc) return rc;
+    return scene_render(sc, camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, row_begin, row_end, 1,
+                        first_sample, nsamples, mode, d_counters, stream);
+}
+
+extern "C" int spt_scene_render_groups_async(const spt_scene *sc, const rt_camera *camera, float *d_colors,
+                                             const uint32_t *d_seeds_in, uint32_t *d_seeds_out, uint32_t *d_pixels,
+                                             int w, int h, int group, int ngroups, int first_sample, int nsamples,
+                                             int mode, uint64_t *d_counters, void *stream)
+{
+    if (!sc) return rtrt::fail(RT_ERR_INVALID, "spt_scene_render_groups_async: null scene");
+    if (ngroups < 1 || group < 0 || group >= ngroups)
+        return rtrt::fail(RT_ERR_INVALID, "spt_scene_render_groups_async: need 0 <= group < ngroups");
+    int rc = check_render_args(camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, 0, h, first_sample,
+                               nsamples, mode);
+    if (rc) return rc;
+    return scene_render(sc, camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, 8 * group, h, ngroups,
+                        first_sample, nsamples, mode, d_counters, stream);
 }
 
 // Device-pointer-only entry: stages the spheres through a cached scene

@@ -17,7 +17,8 @@ SPT_PATH_TRACING, SPT_DIRECT_LIGHTING = 0, 1
 # Every symbol include/rt_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = ("rt_last_error", "rt_device_count", "rt_set_device", "rt_release", "rt_cached_bytes",
            "rtw_render", "rtw_render_async", "rtw_render_ocl", "rtw_render_ocl_async", "spt_render", "spt_render_async", "spt_seed_fill",
-           "spt_scene_create", "spt_scene_destroy", "spt_scene_render_async", "spt_pack_pixels_async",
+           "spt_scene_create", "spt_scene_destroy", "spt_scene_render_async", "spt_scene_render_groups_async",
+           "spt_pack_pixels_async",
            "spt_multi_create", "spt_multi_destroy", "spt_multi_set_scene", "spt_multi_bands", "spt_multi_upload",
            "spt_multi_render_async", "spt_multi_gather_async", "spt_multi_sync", "spt_multi_download",
            "spt_multi_read_frame", "spt_multi_counters", "spt_multi_band_buffers", "spt_render_multi",
@@ -96,6 +97,8 @@ def lib():
     L.spt_scene_create.argtypes = [vp, u, C.POINTER(vp)]
     L.spt_scene_destroy.argtypes = [vp]
     L.spt_scene_render_async.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, i, u64p, vp]
+    if hasattr(L, "spt_scene_render_groups_async"):
+        L.spt_scene_render_groups_async.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, i, u64p, vp]
     if hasattr(L, "spt_pack_pixels_async"):   # (absent from older A/B builds under RT_HIP_LIB)
         L.spt_pack_pixels_async.argtypes = [vp, vp, i, i, i, i, vp]
     L.spt_seed_fill.restype = None

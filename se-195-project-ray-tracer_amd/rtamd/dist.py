@@ -16,6 +16,14 @@ colours with the same toInt pack the kernel ends with (pack callback:
 spt_pack_pixels_async on the GPU), bit-identical to the bands the other ranks
 wrote.  Without a pack callback (CPU tests) the pixel bands are all-gathered
 too.
+
+Interleaved layout (GroupGather, the default of bench.py for N > 1): rank k
+renders the 8-row groups k, k + world, k + 2*world, ...
+(spt_scene_render_groups_async).  Contiguous bands differ in cost with their
+content (at N = 4 the band holding the glass sphere takes 5.8 ms, the others
+5.2 ms); interleaved groups give every GPU the same mix.  The shares are
+packed into one padded buffer each, all-gathered once, and scattered back
+into the frame (exact copies).
 """
 import torch
 import torch.distributed as dist
@@ -60,3 +68,49 @@ def gather_seeds(seeds, rank, world, w, h, group=None):
         return
     B = h // world
     dist.all_gather_into_tensor(seeds, seeds.view(world, 2 * B * w)[rank].clone(), group=group)
+
+
+def group_rows(rank, world, h):
+    """Pixel rows of `rank` in the interleaved split: the 8-row groups g with
+    g % world == rank (the window of spt_scene_render_groups_async)."""
+    return [y for g in range(rank, (h + 7) // 8, world) for y in range(8 * g, min(8 * g + 8, h))]
+
+
+class GroupGather:
+    """FrameGather for the interleaved split: every rank ends with the whole
+    frame -- colors (float32[3*w*h], flipped slots) and pixels (int32[w*h])."""
+
+    def __init__(self, colors, pixels, rank, world, w, h, pack=None):
+        self.rank, self.world, self.w, self.h = rank, world, w, h
+        self.pack = pack
+        dev = colors.device
+        rows = [group_rows(k, world, h) for k in range(world)]
+        self.maxr = max(len(r) for r in rows)
+        self.col2d = colors.view(h, 3 * w)                 # row h-1-y holds pixel row y
+        self.px2d = pixels.view(h, w)
+        slot = lambda k: torch.tensor([h - 1 - y for y in rows[k]], dtype=torch.long, device=dev)  # noqa: E731
+        self.my_slots = slot(rank)
+        self.my_rows = torch.tensor(rows[rank], dtype=torch.long, device=dev)
+        self.all_slots = torch.cat([slot(k) for k in range(world)])
+        self.all_rows = torch.tensor([y for k in range(world) for y in rows[k]], dtype=torch.long, device=dev)
+        self.valid = torch.tensor([k * self.maxr + j for k in range(world) for j in range(len(rows[k]))],
+                                  dtype=torch.long, device=dev)
+        self.n_mine = len(rows[rank])
+        self.send = torch.zeros(self.maxr, 3 * w, dtype=colors.dtype, device=dev)
+        self.recv = torch.empty(world * self.maxr, 3 * w, dtype=colors.dtype, device=dev)
+        if pack is None:
+            self.psend = torch.zeros(self.maxr, w, dtype=pixels.dtype, device=dev)
+            self.precv = torch.empty(world * self.maxr, w, dtype=pixels.dtype, device=dev)
+
+    def gather(self, group=None):
+        if self.world == 1:
+            return
+        torch.index_select(self.col2d, 0, self.my_slots, out=self.send[:self.n_mine])
+        dist.all_gather_into_tensor(self.recv, self.send, group=group)
+        self.col2d.index_copy_(0, self.all_slots, self.recv.index_select(0, self.valid))
+        if self.pack is not None:
+            self.pack()
+        else:
+            torch.index_select(self.px2d, 0, self.my_rows, out=self.psend[:self.n_mine])
+            dist.all_gather_into_tensor(self.precv, self.psend, group=group)
+            self.px2d.index_copy_(0, self.all_rows, self.precv.index_select(0, self.valid))

@@ -130,3 +130,39 @@ def test_multi_bad_arguments(rt):
         rt.SmallptMulti(64, 4, [0] * 5, S, n)       # more bands than rows
     with pytest.raises(rt.RTError):
         rt.SmallptMulti(64, 64, [rt.device_count()], S, n)
+
+
+@pytest.mark.parametrize("ngroups,w,h,spp", [(2, 320, 240, 3), (3, 197, 241, 2), (4, 1920, 1080, 2), (8, 160, 60, 4)])
+def test_interleaved_groups_partition_the_frame(rt, ngroups, w, h, spp):
+    """spt_scene_render_groups_async for groups 0..ngroups-1 (the interleaved
+    multi-GPU split of bench.py) into one device frame == one full-frame
+    render, bit for bit, counters summed."""
+    import ctypes as C
+    import torch
+    dev = torch.device("cuda", 0)
+    S, n = rt.scenes.cornell()
+    cam = rt.scenes.cornell_camera(w, h)
+    sc = rt.SmallptScene(S, n)
+    seeds0 = torch.from_numpy(rt.scenes.seeds(w, h).view(np.int32)).to(dev)
+    L = rt.lib()
+    st = torch.cuda.current_stream(dev)
+
+    def buffers():
+        return (torch.zeros(3 * w * h, dtype=torch.float32, device=dev), torch.empty_like(seeds0),
+                torch.zeros(w * h, dtype=torch.int32, device=dev), torch.zeros(4, dtype=torch.int64, device=dev))
+
+    c1, s1, p1, n1 = buffers()
+    rt.check(L.spt_scene_render_async(sc.handle, C.byref(cam), c1.data_ptr(), seeds0.data_ptr(), s1.data_ptr(),
+                                      p1.data_ptr(), w, h, 0, h, 0, spp, 0, n1.data_ptr(), st.cuda_stream))
+    c2, s2, p2, n2 = buffers()
+    for g in range(ngroups):
+        rt.check(L.spt_scene_render_groups_async(sc.handle, C.byref(cam), c2.data_ptr(), seeds0.data_ptr(),
+                                                 s2.data_ptr(), p2.data_ptr(), w, h, g, ngroups, 0, spp, 0,
+                                                 n2.data_ptr(), st.cuda_stream))
+    torch.cuda.synchronize()
+    assert torch.equal(c1.view(torch.int32), c2.view(torch.int32))
+    assert torch.equal(s1, s2) and torch.equal(p1, p2)
+    assert n1.tolist() == n2.tolist()
+    assert rt.lib().spt_scene_render_groups_async(sc.handle, C.byref(cam), c2.data_ptr(), seeds0.data_ptr(),
+                                                  s2.data_ptr(), p2.data_ptr(), w, h, ngroups, ngroups, 0, 1, 0,
+                                                  None, st.cuda_stream) == rt._lib.RT_ERR_INVALID

@@ -38,3 +38,17 @@ for N in (2, 4, 8):
             best = min(best, a.elapsed_time(b))
         ts.append(best)
     print("N=%d band ms: %s  max/mean %.3f" % (N, " ".join("%.2f" % t for t in ts), max(ts) / np.mean(ts)))
+    ts = []
+    for r in range(N):                     # interleaved 8-row groups (bench.py's default split)
+        best = 1e9
+        for _ in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            rtamd.check(L.spt_scene_render_groups_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                                        seeds.data_ptr(), px.data_ptr(), W, H, r, N, 0, SPP, 0,
+                                                        None, st.cuda_stream))
+            b.record(st)
+            torch.cuda.synchronize()
+            best = min(best, a.elapsed_time(b))
+        ts.append(best)
+    print("N=%d group ms: %s  max/mean %.3f" % (N, " ".join("%.2f" % t for t in ts), max(ts) / np.mean(ts)))
