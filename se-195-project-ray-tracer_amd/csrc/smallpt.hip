@@ -1079,7 +1079,13 @@ Shape launch_shape(const spt_scene &sc, int w, int r0, int r1, int gstride = 1)
     g.gstride = gstride;
     const int groups = (r1 - r0 + 7) / 8;
     g.ntiles = g.tiles_x * ((groups + gstride - 1) / gstride);
-    g.wpb = g.ntiles <= 16 * sc.cus ? 16 : 4;
+    // Waves of work per SIMD: up to 4 (an N = 8 band) run as one round of the
+    // 16-wave block shape (four waves per SIMD, one block per CU); 6..8 (an
+    // N = 4 band: 7.97) as two such rounds -- at occupancy 6 they run as a
+    // full round of 6 and a tail of 2 (N = 4 bands 5.25-5.87 ms -> 5.44-5.47
+    // ms); otherwise 256-thread blocks at the kernel's occupancy.
+    const double wps = (double)g.ntiles / (4.0 * sc.cus);
+    g.wpb = (wps <= 4.0 || (wps > 6.0 && wps <= 8.0)) ? 16 : 4;
     if (const char *e = getenv("RT_SPT_WPB")) g.wpb = atoi(e) == 16 ? 16 : 4;   // A/B
     g.nblocks = (g.ntiles + g.wpb - 1) / g.wpb;
     return g;
