@@ -10,6 +10,7 @@ mkdir -p $D
 cp $S/bench.json $D/bench.json
 cp $S/stats/bench_kernel_stats.csv $D/bench_kernel_stats.csv
 cp $S/pmc_digest.json $D/pmc_digest.json
+[ -f $S/bands_kernel_stats.csv ] && cp $S/bands_kernel_stats.csv $D/bands_kernel_stats.csv
 for d in $S/pmc*/; do
   n=$(basename $d)
   f=$(ls $d/*counter_collection.csv)
