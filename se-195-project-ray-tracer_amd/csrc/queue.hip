@@ -470,6 +470,7 @@ struct QArgs {
     float4 *ncol;         // node term.xyz, counter word (bits)
     int2 *nchild;         // pool slots of the node's children (levels 1..4)
     int *count;           // [C_TOTAL * CSTRIDE]
+    int *ovf;             // host-mapped flag: set when this frame's pool overflowed
     int pool, fixcap, ntrees, npix, w;
     int row_begin, row_stride;   // the slab's rows: see slab_row
 };
@@ -771,6 +772,16 @@ fix_kernel(QArgs A, float DX, float DY, uint32_t *__restrict__ out, unsigned lon
 {
     const int nfix = QCNT(A, C_FIX);
     if (nfix == 0) return;
+    if (blockIdx.x == 0) {
+        // A segment counter past its limit: the pool was too small (the next
+        // frame gets a larger one).
+        bool over = false;
+        for (int L = 1; L < LEVELS; L++) {
+            const int base = level_base(A, L);
+            over = over || QCNT(A, C_SEG + L * lq::NSEG + (int)threadIdx.x) > lq::seg_limit(A.pool, base);
+        }
+        if (__builtin_amdgcn_ballot_w64(over) != 0 && threadIdx.x == 0) *(volatile int *)A.ovf = 1;
+    }
     __shared__ Scene S;
     __shared__ int ring[RING][64];
     load_scene(S, A.scene);
@@ -834,7 +845,7 @@ constexpr int SLOT_Q = 8;       // rtrt scratch slot of the queue tracer's arena
 // them: the reference scene needs 0.70 (3.02 M nodes below the roots for
 // 4.32 M trees at 800 x 600); a tree with a node that does not fit is
 // re-evaluated by final_kernel, exactly, so a denser scene is slower, never
-// wrong.
+// wrong (and the next frame's pool is 1.25x larger: rtrt::pool_fraction).
 constexpr long long SLAB_TREES = 12000000;
 constexpr double POOL_FRAC = 0.9;
 
@@ -851,7 +862,8 @@ int arena(rtrt::DeviceState &st, int w, int rows, rt::queue::QArgs *A)
     using namespace rt::queue;
     const size_t T = (size_t)w * rows * NSUB;
     if (T > (size_t)0x7fffffff / 2) return rtrt::fail(RT_ERR_INVALID, "rtq: frame too large");
-    size_t P = (size_t)(T * POOL_FRAC);
+    int *ovf = nullptr;
+    size_t P = (size_t)(T * rtrt::pool_fraction(st, rtrt::POOL_QUEUE, (long long)T, POOL_FRAC, &ovf));
     if (const char *e = getenv("RT_QUEUE_POOL_CAP")) {      // test hook: exercises the overflow path
         const long long v = atoll(e);
         if (v > 0 && (size_t)v < P) P = (size_t)v;
@@ -886,6 +898,7 @@ int arena(rtrt::DeviceState &st, int w, int rows, rt::queue::QArgs *A)
     A->nchild = (int2 *)take(P * 8);
     A->count = (int *)take(sizeof(int) * C_TOTAL * rt::lq::CSTRIDE);
     if ((size_t)(p - (char *)base) > bytes) return rtrt::fail(RT_ERR_INVALID, "rtq: arena layout exceeds its size");
+    A->ovf = ovf;
     A->pool = (int)P;
     A->fixcap = (int)FC;
     A->w = w;

@@ -82,6 +82,16 @@ int state(DeviceState **out)
             delete st;
             return fail_hip(e, "hipEventCreate");
         }
+        e = hipHostMalloc((void **)&st->pool_ovf, POOL_FITS * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&st->pool_ovf_dev, st->pool_ovf, 0);
+        if (e != hipSuccess) {
+            (void)hipEventDestroy(st->wf_done);
+            (void)hipStreamDestroy(st->stream);
+            if (st->pool_ovf) (void)hipHostFree(st->pool_ovf);
+            delete st;
+            return fail_hip(e, "hipHostMalloc");
+        }
+        memset(st->pool_ovf, 0, POOL_FITS * sizeof(int));
         g_states[dev] = st;
     } else {
         hipError_t e = hipSetDevice(dev);
@@ -111,6 +121,35 @@ int scratch(DeviceState &st, int slot, size_t bytes, void **out)
     }
     *out = st.buf[slot];
     return RT_OK;
+}
+
+double pool_fraction(DeviceState &st, int which, long long trees, double initial, int **flag_dev)
+{
+    int i = 0;
+    while (i < POOL_FITS && !(st.pool_fit[i].which == which && st.pool_fit[i].trees == trees)) i++;
+    volatile int *flag;
+    if (i == POOL_FITS) {                          // a new size: replace the oldest entry
+        i = st.pool_fit_next;
+        st.pool_fit_next = (i + 1) % POOL_FITS;
+        st.pool_fit[i].which = which;
+        st.pool_fit[i].trees = trees;
+        st.pool_fit[i].frac = initial;
+        if (const char *e = getenv("RT_POOL_FRAC")) {      // test hook: a small first pool (it overflows)
+            const double v = atof(e);
+            if (v > 0.0 && v < POOL_FRAC_MAX) st.pool_fit[i].frac = v;
+        }
+        flag = st.pool_ovf + i;
+        *flag = 0;
+    } else {
+        flag = st.pool_ovf + i;
+        if (*flag) {
+            *flag = 0;
+            const double f = st.pool_fit[i].frac * 1.25;
+            st.pool_fit[i].frac = f < POOL_FRAC_MAX ? f : POOL_FRAC_MAX;
+        }
+    }
+    *flag_dev = st.pool_ovf_dev + i;
+    return st.pool_fit[i].frac;
 }
 
 int thread_device() { return g_dev; }

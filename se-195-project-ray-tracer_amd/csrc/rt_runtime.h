@@ -34,7 +34,22 @@ struct DeviceState {
     int vt_w = 0, vt_h = 0, vt_ocl = -1;
     hipEvent_t wf_done = nullptr;
     bool wf_pending = false;
+    // Record pools of the level passes (POOL_WHITTED, POOL_QUEUE) as a
+    // fraction of a slab's trees, learnt per (pass, slab size).  A frame whose
+    // nodes did not all fit (the trees left over are re-evaluated exactly by
+    // the fixup kernels, one lane per tree: correct but slow) raises its
+    // entry's flag in host-mapped memory (pool_ovf, written by the fixup
+    // kernel); the next frame of that size then sizes its pool 1.25x larger
+    // (pool_fraction).
+    struct PoolFit { int which = -1; long long trees = 0; double frac = 0.0; };
+    PoolFit pool_fit[16];
+    int pool_fit_next = 0;
+    int *pool_ovf = nullptr;           // host-mapped [16]
+    int *pool_ovf_dev = nullptr;       // its device address
 };
+
+constexpr int POOL_WHITTED = 0, POOL_QUEUE = 1, POOL_FITS = 16;
+constexpr double POOL_FRAC_MAX = 8.0;
 
 // Records msg (plus the HIP error string) for rt_last_error(); returns code.
 int fail(int code, const char *msg);
@@ -45,6 +60,10 @@ int check_launch(const char *what);
 int state(DeviceState **out);
 // Device buffer slot `slot` of at least `bytes` (grow-only, reused).
 int scratch(DeviceState &st, int slot, size_t bytes, void **out);
+// Pool fraction of level pass `which` for the next frame of `trees` trees
+// per slab (starts at `initial`; grown after an overflowed frame of that
+// size) and, in *flag_dev, the device address of that entry's overflow flag.
+double pool_fraction(DeviceState &st, int which, long long trees, double initial, int **flag_dev);
 // The calling thread's rt_set_device choice (-1: none, HIP's current device).
 int thread_device();
 // Saves the calling thread's device selection (rt_set_device and HIP's

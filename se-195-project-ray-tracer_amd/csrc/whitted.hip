@@ -421,6 +421,7 @@ struct WfArgs {
     int2 *lchild;             // pool slots of the node's children
     int4 *tir[LEVELS];        // [tcap] TIR nodes of level L (0..4): slot, tree, node, rindex (bits)
     int *count;               // [C_TOTAL * CSTRIDE]
+    int *ovf;                 // host-mapped flag: set when this frame's pool or a TIR list overflowed
     int pool, fixcap, tcap, ntrees, npix, w;
     int row_begin, row_stride;   // the slab's rows: see slab_row
     int side, nsub;           // sub-sample grid: 3 x 3 (CPU path) or 2 x 2 (openCLcode.cl)
@@ -792,6 +793,18 @@ fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict
     __shared__ Scene S;
     load_scene(S, A.scene);
     const int nfix = CNT(A, C_FIX);
+    if (blockIdx.x == 0 && nfix > 0) {
+        // Tell the host when a queue asked for more than its pages (a segment
+        // counter past its limit) or a TIR list for more than its capacity:
+        // the next frame gets a larger pool.
+        const int lane = threadIdx.x;
+        bool over = lane < LEVELS - 1 && CNT(A, C_TIR + lane) > A.tcap;
+        for (int L = 1; L < LEVELS; L++) {
+            const int base = level_base(A, L);
+            over = over || CNT(A, C_SEG + L * NSEG + lane) > seg_limit(A, base);
+        }
+        if (__builtin_amdgcn_ballot_w64(over) != 0 && lane == 0) *(volatile int *)A.ovf = 1;
+    }
     const bool scan = nfix > A.fixcap;                  // the list overflowed: walk the bitmask
     const int nitems = scan ? (A.ntrees + 31) >> 5 : nfix;
     Counts cnt = {0, 0, 0, 0};
@@ -909,10 +922,12 @@ constexpr int SLOT_WF = 6;      // rtrt scratch slot of the level-pass arena
 // interleave in groups of 16 rows (slab_row), so every slab holds the
 // frame's mix of sphere / plane / background rows and so its queue fill.
 constexpr long long SLAB_TREES = 18000000;
-// Record pool (levels 1..5 together) as a fraction of the slab's trees.  The
-// reference scene needs 0.83 (14.2 M nodes for 17.1 M trees at 1080p); a
-// tree whose node does not fit is finished by fixup_kernel, exactly, so a
-// denser scene is slower, never wrong.
+// Record pool (levels 1..5 together) as a fraction of the slab's trees, to
+// start with.  The reference scene needs 0.83 at 1080p (14.2 M nodes for
+// 17.1 M trees) but 0.94 at 640 x 480 (its rows [20, 410) hold more of the
+// spheres); a tree whose node does not fit is finished by fixup_kernel,
+// exactly but ~5x slower per frame, and the next frame's pool is 1.25x
+// larger (rtrt::pool_fraction), so a denser scene costs a frame or two.
 constexpr double POOL_FRAC = 0.9;
 
 // m_SX / m_SY (Engine_InitRender raytracer.cpp:278-294, then the sequential
@@ -987,7 +1002,8 @@ int wavefront_arena(rtrt::DeviceState &st, int w, int rows, int nsub, rt::whitte
     if (T > (size_t)0x7fffffff / 2) return rtrt::fail(RT_ERR_INVALID, "rtw: frame too large");
     // RT_WHITTED_QUEUE_CAP lowers the pool (test hook: exercises the
     // overflow -> fixup path).
-    size_t P = (size_t)(T * POOL_FRAC);
+    int *ovf = nullptr;
+    size_t P = (size_t)(T * rtrt::pool_fraction(st, rtrt::POOL_WHITTED, (long long)T, POOL_FRAC, &ovf));
     if (const char *e = getenv("RT_WHITTED_QUEUE_CAP")) {
         const long long v = atoll(e);
         if (v > 0 && (size_t)v < P) P = (size_t)v;
@@ -1020,6 +1036,7 @@ int wavefront_arena(rtrt::DeviceState &st, int w, int rows, int nsub, rt::whitte
     A->lchild = (int2 *)take(P * 8);
     for (int L = 0; L < LEVELS; L++) A->tir[L] = L < LEVELS - 1 ? (int4 *)take(TC * 16) : nullptr;
     A->count = (int *)take(sizeof(int) * C_TOTAL * CSTRIDE);
+    A->ovf = ovf;
     A->pool = (int)P;
     A->fixcap = (int)FC;
     A->tcap = (int)TC;

@@ -83,6 +83,22 @@ def test_pool_overflow_reevaluates_exactly(rt, cap, monkeypatch):
     assert (px == r2).all() and cnt == c2
 
 
+def test_pool_grows_after_overflow(rt, monkeypatch):
+    """A first pool far too small (RT_POOL_FRAC): the overflowed frame is
+    exact and flags the overflow to the host; the following frames of that
+    size get a pool 1.25x larger each time (the arena grows), all exact."""
+    monkeypatch.setenv("RT_POOL_FRAC", "0.2")
+    w, h = 352, 288                     # a size no other test uses: a fresh pool entry
+    ref, rc = O.queue_render(w, h, nthreads=NT)
+    rt.lib().rt_release()
+    sizes = []
+    for _ in range(6):
+        px, cnt = rt.queue_render(w, h, counters=True)
+        assert (px == ref).all() and cnt == rc
+        sizes.append(rt.lib().rt_cached_bytes())
+    assert sizes[-1] > sizes[0], sizes
+
+
 def test_exact_path_everywhere(rt, monkeypatch):
     """RT_QUEUE_EXACT_ALL=1: every specular term is treated as uncertified, so
     nearly every pixel is finished by fix_kernel with glibc's pow restated

@@ -163,3 +163,20 @@ def test_async_frames_on_other_streams_are_ordered(rt, oracle):
         ref, _ = oracle.whitted_render(w, h, nthreads=8)
         got = f.cpu().numpy().view(np.uint32).reshape(h, w)
         assert (got == ref).all(), (w, h)
+
+
+def test_pool_grows_after_overflow(rt, oracle, monkeypatch):
+    """A frame whose nodes overflow the record pool is finished exactly by
+    fixup_kernel and raises the host-mapped overflow flag; the next frames of
+    that size get a pool 1.25x larger each time until it fits (the arena
+    grows).  Every frame bit-exact, counts included."""
+    monkeypatch.setenv("RT_POOL_FRAC", "0.25")
+    w, h = 352, 288                     # a size no other test uses: a fresh pool entry
+    ref, rc = oracle.whitted_render(w, h, nthreads=8)
+    rt.lib().rt_release()
+    sizes = []
+    for _ in range(6):
+        got, gc = rt.whitted_render(w, h, counters=True)
+        assert (got == ref).all() and gc == rc
+        sizes.append(rt.lib().rt_cached_bytes())
+    assert sizes[-1] > sizes[0], sizes

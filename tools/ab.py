@@ -5,7 +5,7 @@ process per variant, interleaved rounds, HIP-event time on the launch stream).
 
 smallpt: Cornell 1920x1080, SPP (default 64) samples per launch; BAND=k/N renders
 only row band k of N (rtamd.dist.row_band: the per-GPU work of an N-GPU frame).
-whitted: raytracer3.0.06 scene, 1920x1080, rows [20, H-70).
+whitted: raytracer3.0.06 scene, 1920x1080 (WH=640x480: configs[0]'s size), rows [20, H-70).
 """
 import ctypes as C
 import os
@@ -20,7 +20,7 @@ def child():
     import numpy as np
     import torch
     import rtamd
-    W, H = 1920, 1080
+    W, H = (int(v) for v in os.environ.get("WH", "1920x1080").split("x"))
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
     L = rtamd.lib()
@@ -53,7 +53,8 @@ def child():
             rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
                                                  seeds.data_ptr(), px.data_ptr(), W, H, r0, r1, 0, SPP, 0,
                                                  None, st.cuda_stream))
-    run()
+    for _ in range(int(os.environ.get("WARM", "1"))):
+        run()
     torch.cuda.synchronize()
     ts = []
     for _ in range(int(os.environ.get("REPS", "5"))):
