@@ -261,9 +261,7 @@ constexpr float BVH_ALPHA_R = 1.f / 64.f;   // per node, with BETA, in the node 
 #ifndef RT_BVH_K
 #define RT_BVH_K 2.f
 #endif
-#ifndef RT_BVH_BATCH
-#define RT_BVH_BATCH 32     // leaf postponement: test pending leaves once >= BATCH/64 of the walking lanes hold one
-#endif
+
 #ifndef RT_BVH_LEAF_BF
 #define RT_BVH_LEAF_BF 1    // branch-free leaf sphere tests (configs[4] 40.5 -> 39.5 ms; 0 = per-sphere branch, A/B)
 #endif
@@ -305,7 +303,23 @@ __device__ unsigned long long g_bvh_stats[24];
 // continues).  t = nearest distance so far (any hit: maxt, unchanged), id =
 // the result so far, node = next node in the ray's octant layout (nnodes:
 // finished), pend = a crossed leaf not yet tested (first | count << 24).
-struct BvhWalk { float t; int id, node, pend; };
+#ifndef RT_BVH_PEND2
+#define RT_BVH_PEND2 1      // a lane may hold two crossed leaves and keeps stepping while it holds one
+#endif
+#ifndef RT_BVH_BATCH        // leaf postponement: test pending leaves once >= BATCH/64 of the lanes in the walk
+#if RT_BVH_PEND2            //   cannot step (hold two leaves, or reached the end with one) -- else: hold one
+#define RT_BVH_BATCH 16
+#else
+#define RT_BVH_BATCH 32
+#endif
+#endif
+struct BvhWalk {
+    float t;
+    int id, node, pend;
+#if RT_BVH_PEND2
+    int pend2;              // a second crossed leaf (only while pend holds one)
+#endif
+};
 
 // Starts a query: the "always" spheres, then the walk from the root.
 // Nearest hit (shadow = false): t = 1e20f on entry; any hit: t = maxt.
@@ -328,6 +342,9 @@ __device__ __forceinline__ void bvh_begin(const BvhView &B, const ray3 &r, bool 
     W.id = id;
     W.node = (!COUNT && shadow && id >= 0) ? B.nnodes : 0;
     W.pend = 0;
+#if RT_BVH_PEND2
+    W.pend2 = 0;
+#endif
 }
 
 // Advances the walks of the wave's lanes by up to RT_BVH_BUDGET steps
@@ -347,6 +364,11 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
     const float maxt = W.t;
     float t = W.t;
     int id = W.id, node = W.node, pend = W.pend;
+#if RT_BVH_PEND2
+    int pend2 = W.pend2;
+#else
+    constexpr int pend2 = 0;
+#endif
     // Slab test (culling only: its rounding is inside the margin; fused ops
     // are fine here and nowhere else).  Zero direction components become
     // +-1e-30 so no 0 * inf appears.
@@ -359,16 +381,18 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
     // Layout of this ray's direction octant: near children first.  A 32-bit
     // element offset from the uniform base (one VGPR, not a 64-bit pointer).
     const unsigned lay = 2u * (unsigned)B.nnodes * ((dx < 0.f ? 1u : 0u) | (dy < 0.f ? 2u : 0u) | (dz < 0.f ? 4u : 0u));
-    // Crossed leaves are postponed: a lane that reaches one stops stepping
-    // and keeps it pending; the wave tests the pending leaves' spheres
-    // together once at least RT_BVH_BATCH/64 of its lanes still in the walk
-    // hold one (or none can step), instead of running the leaf block for the
-    // one or two lanes that reach a leaf in a given step.  The result does
-    // not depend on the order spheres are tested in (minimum, ties to the
-    // highest index; or "some occluder").
+    // Crossed leaves are postponed: a lane that reaches one keeps it pending
+    // and steps on until it holds a second (RT_BVH_PEND2; else it stops at
+    // the first); the wave tests one pending leaf per lane together once at
+    // least RT_BVH_BATCH/64 of its lanes still in the walk cannot step (or
+    // none can), instead of running the leaf block for the one or two lanes
+    // that reach a leaf in a given step.  The result does not depend on the
+    // order spheres are tested in (minimum, ties to the highest index; or
+    // "some occluder"); a leaf tested later than it was crossed only makes
+    // the culling limit t of the steps in between looser, never wrong.
     int trips = 0;
     while (true) {
-        if (node < B.nnodes && pend == 0) {
+        if (node < B.nnodes && (RT_BVH_PEND2 ? pend2 == 0 : pend == 0)) {
             BVH_ST(0, 1);
             BVH_ST(21, node < 64);
             BVH_ST(22, node < 256);
@@ -388,20 +412,34 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
             int next = cross ? node + 1 : link;
             if (link < 0) {                              // leaf ~(first | count << 24); escape = next node
                 next = node + 1;
+#if RT_BVH_PEND2
+                if (cross) {
+                    if (pend == 0) pend = ~link;
+                    else pend2 = ~link;
+                }
+#else
                 if (cross) pend = ~link;
+#endif
             }
             node = next;
         }
         trips++;
         const unsigned long long pm = __builtin_amdgcn_ballot_w64(pend != 0);
-        const unsigned long long sm = __builtin_amdgcn_ballot_w64(node < B.nnodes && pend == 0);
+        const unsigned long long sm = __builtin_amdgcn_ballot_w64(node < B.nnodes && (RT_BVH_PEND2 ? pend2 == 0 : pend == 0));
         if (pm == 0) {
             if (sm == 0 || trips >= RT_BVH_BUDGET) break;
             continue;
         }
+#if RT_BVH_PEND2
+        // leaves tested once half the lanes in the walk cannot step
+        if (sm != 0 && trips < RT_BVH_BUDGET &&
+            64 * __builtin_popcountll(pm & ~sm) < RT_BVH_BATCH * __builtin_popcountll(pm | sm))
+            continue;
+#else
         if (sm != 0 && trips < RT_BVH_BUDGET &&
             64 * __builtin_popcountll(pm) < RT_BVH_BATCH * __builtin_popcountll(pm | sm))
             continue;
+#endif
         if (pend != 0) {
             const int f = pend & 0xffffff, c = pend >> 24;
             BVH_ST(1, 1);
@@ -475,8 +513,17 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
                 }
             }
 #endif
+#if RT_BVH_PEND2
+            if (!COUNT && shadow && id >= 0) {
+                node = B.nnodes;
+                pend2 = 0;
+            }
+            pend = pend2;
+            pend2 = 0;
+#else
             if (!COUNT && shadow && id >= 0) node = B.nnodes;
             pend = 0;
+#endif
         }
         if (trips >= RT_BVH_BUDGET) break;
     }
@@ -484,6 +531,9 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
     W.id = id;
     W.node = node;
     W.pend = pend;
+#if RT_BVH_PEND2
+    W.pend2 = pend2;
+#endif
 #ifdef RT_BVH_STATS
     {
         const float4 a0 = B.node[lay], b0 = B.node[lay + 1u];
