@@ -142,8 +142,10 @@ int spt_render(const rt_sphere *spheres, unsigned nspheres, const rt_camera *cam
  * are full-frame device arrays laid out as above; seeds are read from
  * d_seeds_in and the advanced state written to d_seeds_out (may alias).
  * camera is read on the host at call time (passed by value to the kernel).
- * Reads the sphere array back once to prepare it and synchronises `stream`
- * before returning; use spt_scene_* to stay fully asynchronous. */
+ * Reads the sphere array back (synchronising `stream` once) to find or
+ * prepare the device's cached scene -- prepared again only when the array's
+ * contents change -- then launches asynchronously; use spt_scene_* to stay
+ * fully asynchronous.  spt_render uses the same cache. */
 int spt_render_async(const rt_sphere *d_spheres, unsigned nspheres, const rt_camera *camera,
                      float *d_colors, const uint32_t *d_seeds_in, uint32_t *d_seeds_out,
                      uint32_t *d_pixels, int w, int h, int row_begin, int row_end,

@@ -196,6 +196,7 @@ extern "C" int rt_set_device(int device)
 
 extern "C" int rt_release(void)
 {
+    rtrt::release_cached_scenes();
     std::lock_guard<std::mutex> lk(rtrt::g_mu);
     for (int d = 0; d < 64; d++) {
         if (rtrt::g_states[d]) {

@@ -64,6 +64,9 @@ int scratch(DeviceState &st, int slot, size_t bytes, void **out);
 // per slab (starts at `initial`; grown after an overflowed frame of that
 // size) and, in *flag_dev, the device address of that entry's overflow flag.
 double pool_fraction(DeviceState &st, int which, long long trees, double initial, int **flag_dev);
+// Frees the per-device scenes cached by spt_render / spt_render_async
+// (smallpt.hip; rt_release).
+void release_cached_scenes();
 // The calling thread's rt_set_device choice (-1: none, HIP's current device).
 int thread_device();
 // Saves the calling thread's device selection (rt_set_device and HIP's

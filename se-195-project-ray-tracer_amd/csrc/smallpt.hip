@@ -1094,6 +1094,7 @@ __global__ void __launch_bounds__(256) pack_kernel(const float *__restrict__ col
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <string>
 #include <vector>
 #include "rt_runtime.h"
 
@@ -1521,8 +1522,65 @@ extern "C" int spt_scene_render_groups_async(const spt_scene *sc, const rt_camer
                         first_sample, nsamples, mode, d_counters, stream);
 }
 
-// Device-pointer-only entry: stages the spheres through a cached scene
-// object (one D2H read of the sphere array per new pointer/size).
+namespace {
+// One prepared scene per device for the entry points that take a bare sphere
+// array (spt_render, spt_render_async), reused while the array is unchanged
+// (compared byte for byte): a progressive loop calling them once per pass no
+// longer re-uploads the scene, rebuilds its hierarchy (>= 256 spheres) and
+// synchronises the device to free it on every call.
+struct SceneCache {
+    std::vector<rt_sphere> host;
+    std::string hooks;                // the preparation's test hooks (RT_SPT_NO_BVH, RT_SPT_GEO)
+    spt_scene *sc = nullptr;
+};
+SceneCache g_scene_cache[64];
+
+std::string prep_hooks()
+{
+    const char *a = getenv("RT_SPT_NO_BVH"), *b = getenv("RT_SPT_GEO");
+    return std::string(a ? "1" : "0") + "|" + (b ? b : "");
+}
+
+// Caller holds the device state's lock.
+int cached_scene(const rtrt::DeviceState &st, const rt_sphere *spheres, unsigned n, spt_scene **out)
+{
+    SceneCache &c = g_scene_cache[st.device];
+    const std::string hooks = prep_hooks();
+    if (c.sc && c.host.size() == n && c.hooks == hooks &&
+        memcmp(c.host.data(), spheres, sizeof(rt_sphere) * n) == 0) {
+        *out = c.sc;
+        return RT_OK;
+    }
+    if (c.sc) {
+        spt_scene_destroy(c.sc);          // waits for the frames that use it
+        c.sc = nullptr;
+        c.host.clear();
+    }
+    int rc = spt_scene_create(spheres, n, &c.sc);
+    if (rc) {
+        c.sc = nullptr;
+        return rc;
+    }
+    c.host.assign(spheres, spheres + n);
+    c.hooks = hooks;
+    *out = c.sc;
+    return RT_OK;
+}
+}  // namespace
+
+namespace rtrt {
+void release_cached_scenes()
+{
+    for (SceneCache &c : g_scene_cache) {
+        if (c.sc) spt_scene_destroy(c.sc);
+        c.sc = nullptr;
+        c.host.clear();
+    }
+}
+}  // namespace rtrt
+
+// Device-pointer-only entry: reads the sphere array back (one sync of
+// `stream`) to find or prepare the cached scene, then renders asynchronously.
 extern "C" int spt_render_async(const rt_sphere *d_spheres, unsigned nspheres, const rt_camera *camera,
                                 float *d_colors, const uint32_t *d_seeds_in, uint32_t *d_seeds_out,
                                 uint32_t *d_pixels, int w, int h, int row_begin, int row_end,
@@ -1534,21 +1592,18 @@ extern "C" int spt_render_async(const rt_sphere *d_spheres, unsigned nspheres, c
     int rc = check_render_args(camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, row_begin,
                                row_end, first_sample, nsamples, mode);
     if (rc) return rc;
+    rtrt::DeviceState *st;
+    if ((rc = rtrt::state(&st))) return rc;
+    std::lock_guard<std::recursive_mutex> lk(st->mu);
     std::vector<rt_sphere> host(nspheres);
     hipError_t e = hipMemcpyAsync(host.data(), d_spheres, sizeof(rt_sphere) * nspheres, hipMemcpyDeviceToHost,
                                   (hipStream_t)stream);
     if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
     if (e != hipSuccess) return rtrt::fail_hip(e, "spt_render_async scene read");
     spt_scene *sc;
-    if ((rc = spt_scene_create(host.data(), nspheres, &sc))) return rc;
-    rc = spt_scene_render_async(sc, camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, row_begin,
-                                row_end, first_sample, nsamples, mode, d_counters, stream);
-    if (rc == RT_OK) {
-        e = hipStreamSynchronize((hipStream_t)stream);
-        if (e != hipSuccess) rc = rtrt::fail_hip(e, "spt_render_async");
-    }
-    spt_scene_destroy(sc);
-    return rc;
+    if ((rc = cached_scene(*st, host.data(), nspheres, &sc))) return rc;
+    return spt_scene_render_async(sc, camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, row_begin,
+                                  row_end, first_sample, nsamples, mode, d_counters, stream);
 }
 
 extern "C" int spt_pack_pixels_async(const float *d_colors, uint32_t *d_pixels, int w, int h, int row_begin,
@@ -1605,6 +1660,7 @@ extern "C" int spt_render(const rt_sphere *spheres, unsigned nspheres, const rt_
     rtrt::DeviceState *st;
     int rc = rtrt::state(&st);
     if (rc) return rc;
+    std::lock_guard<std::recursive_mutex> lk(st->mu);
     const size_t npx = (size_t)w * h;
     void *d_col, *d_seed, *d_px, *d_cnt;
     if ((rc = rtrt::scratch(*st, 1, 3 * sizeof(float) * npx, &d_col))) return rc;
@@ -1612,17 +1668,17 @@ extern "C" int spt_render(const rt_sphere *spheres, unsigned nspheres, const rt_
     if ((rc = rtrt::scratch(*st, 3, sizeof(uint32_t) * npx, &d_px))) return rc;
     if ((rc = rtrt::scratch(*st, 4, 4 * sizeof(uint64_t), &d_cnt))) return rc;
     spt_scene *sc;
-    if ((rc = spt_scene_create(spheres, nspheres, &sc))) return rc;
+    if ((rc = cached_scene(*st, spheres, nspheres, &sc))) return rc;
     hipStream_t s = st->stream;
     hipError_t e = hipMemcpyAsync(d_seed, seeds, 2 * sizeof(uint32_t) * npx, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && first_sample > 0)
         e = hipMemcpyAsync(d_col, colors, 3 * sizeof(float) * npx, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && counters) e = hipMemsetAsync(d_cnt, 0, 4 * sizeof(uint64_t), s);
-    if (e != hipSuccess) { spt_scene_destroy(sc); return rtrt::fail_hip(e, "spt_render H2D"); }
+    if (e != hipSuccess) return rtrt::fail_hip(e, "spt_render H2D");
     rc = spt_scene_render_async(sc, camera, (float *)d_col, (uint32_t *)d_seed, (uint32_t *)d_seed,
                                 (uint32_t *)d_px, w, h, 0, h, first_sample, nsamples, mode,
                                 counters ? (uint64_t *)d_cnt : nullptr, s);
-    if (rc) { spt_scene_destroy(sc); return rc; }
+    if (rc) return rc;
     e = hipMemcpyAsync(seeds, d_seed, 2 * sizeof(uint32_t) * npx, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess && nsamples > 0) {
         e = hipMemcpyAsync(colors, d_col, 3 * sizeof(float) * npx, hipMemcpyDeviceToHost, s);
@@ -1631,7 +1687,6 @@ extern "C" int spt_render(const rt_sphere *spheres, unsigned nspheres, const rt_
     if (e == hipSuccess && counters)
         e = hipMemcpyAsync(counters, d_cnt, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    spt_scene_destroy(sc);
     if (e != hipSuccess) return rtrt::fail_hip(e, "spt_render D2H");
     return RT_OK;
 }

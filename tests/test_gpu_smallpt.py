@@ -188,6 +188,38 @@ def test_async_device_paths(rt, oracle):
         assert (seeds == ref[1]).all() and (px == ref[2]).all()
 
 
+def test_scene_cache_follows_the_array(rt, oracle):
+    """spt_render / spt_render_async keep one prepared scene per device while
+    the sphere array is unchanged; a changed array (same size, one sphere's
+    colour and one's position edited in place) is prepared again: every frame
+    equals the oracle's for the array it was given."""
+    import ctypes as C
+    import torch
+    w, h = 64, 48
+    S, n = rt.scenes.cornell()
+    cam = rt.scenes.cornell_camera(w, h)
+    T, _ = rt.scenes.cornell()
+    T[7].c.x, T[8].p.y = 0.25, T[8].p.y + 3.0
+    dev = torch.device("cuda", 0)
+    seeds0 = torch.from_numpy(rt.scenes.seeds(w, h).view(np.int32)).to(dev)
+    d_s = torch.frombuffer(bytearray(bytes(S)), dtype=torch.uint8).to(dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for arr in (S, S, T, S):
+        ref_col, ref_seeds, ref_px, _ = _oracle_frame(oracle, w, h, [2], spheres=(arr, n), cam=cam)
+        d_s.copy_(torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8))     # same pointer, new contents
+        col = torch.zeros(3 * w * h, dtype=torch.float32, device=dev)
+        seeds = torch.zeros_like(seeds0)
+        px = torch.zeros(w * h, dtype=torch.int32, device=dev)
+        rt.check(rt.lib().spt_render_async(d_s.data_ptr(), n, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                           seeds.data_ptr(), px.data_ptr(), w, h, 0, h, 0, 2, 0, None, st))
+        torch.cuda.synchronize()
+        assert (col.cpu().numpy().view(np.uint32) == ref_col.view(np.uint32)).all()
+        assert (seeds.cpu().numpy().view(np.uint32) == ref_seeds).all()
+        f = rt.SmallptFrame(w, h, spheres=arr, nspheres=n, camera=cam)
+        f.render(2, counters=False)
+        assert (f.colors.view(np.uint32) == ref_col.view(np.uint32)).all() and (f.pixels == ref_px).all()
+
+
 def _bvh_vs_scan(rt, monkeypatch, spheres, n, cam, w, h, spp, mode=0):
     """Renders with the hierarchy and with the full scan (RT_SPT_NO_BVH),
     each with and without the work counters (the uncounted kernels stop a
