@@ -337,6 +337,46 @@ def c5_line(args, dev):
     return out
 
 
+def cornell_line(args, dev, w, h, spp, workload):
+    """Side lines: BASELINE configs[2] (Cornell 1024x768, 64 spp) and the
+    per-GPU work of configs[3] (Cornell 1920x1080, 256 spp: one GPU renders
+    the whole frame; the tiled 2/4/8-GPU form is the headline's sharded
+    path) -- one launch per frame from the initial state, HIP events on the
+    launch stream, median of 3 after a warm-up."""
+    spheres, n = rtamd.scenes.cornell()
+    cam = rtamd.scenes.cornell_camera(w, h)
+    sc = rtamd.SmallptScene(spheres, n)
+    seeds0 = torch.from_numpy(rtamd.scenes.seeds(w, h).view(np.int32)).to(dev)
+    seeds = torch.empty_like(seeds0)
+    col = torch.zeros(3 * w * h, dtype=torch.float32, device=dev)
+    px = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev)
+    L = rtamd.lib()
+
+    def run(c=None):
+        rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                             seeds.data_ptr(), px.data_ptr(), w, h, 0, h, 0, spp,
+                                             rtamd.SPT_PATH_TRACING, c.data_ptr() if c is not None else None,
+                                             s.cuda_stream))
+
+    run(cnt)
+    torch.cuda.synchronize(dev)
+    counts = cnt.tolist()
+    ts = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        run()
+        e1.record(s)
+        torch.cuda.synchronize(dev)
+        ts.append(e0.elapsed_time(e1))
+    ms = float(np.median(ts))
+    rays = counts[0] + counts[1]
+    return {"workload": workload, "ms_per_frame": round(ms, 3), "Mrays_per_s": round(rays / ms / 1e3, 2),
+            "Msamples_per_s": round(w * h * spp / ms / 1e3, 2), "rays_per_frame": rays}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -517,6 +557,9 @@ def main():
             out["whitted"] = whitted_line(args, dev)
             out["configs4"] = c5_line(args, dev)
             out["queue3203"] = queue_line(args, dev)
+            out["configs2"] = cornell_line(args, dev, 1024, 768, 64, "configs[2]: Cornell 1024x768, 64 spp, 1 GPU")
+            out["configs3_1gpu"] = cornell_line(args, dev, W, H, 256,
+                                                "configs[3] per-GPU work at N=1: Cornell 1920x1080, 256 spp")
             if not args.no_cpu:
                 out["configs0"] = configs0_line(args, dev)
         out["cpu_baseline"] = None if args.no_cpu else cpu_baseline(args)
