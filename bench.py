@@ -69,7 +69,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--no-whitted", action="store_true", help="skip the Whitted side line")
+    ap.add_argument("--no-whitted", action="store_true", help="skip the side lines")
+    ap.add_argument("--no-cornell-extra", action="store_true",
+                    help="skip the configs[2] / configs[3] lines (other launches of the headline kernel: "
+                         "profiling runs keep its per-launch statistics to the headline frame)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU sample length")
     return ap.parse_args()
 
@@ -377,6 +380,40 @@ def cornell_line(args, dev, w, h, spp, workload):
             "Msamples_per_s": round(w * h * spp / ms / 1e3, 2), "rays_per_frame": rays}
 
 
+def configs3_line(step, cnt, dev, world, distributed, spp=256, frames=2):
+    """BASELINE configs[3]: the Cornell 1920x1080 frame at 256 spp, tiled
+    across the job's GPUs exactly as the headline steps are (each rank renders
+    its rows, then the RCCL all-gather + repack); a counted frame, then
+    `frames` timed frames bracketed by barrier + synchronize, max over ranks."""
+    cnt.zero_()
+    step(counters=cnt, spp=spp)
+    torch.cuda.synchronize(dev)
+    counts = cnt.clone()
+    if distributed:
+        dist.all_reduce(counts)
+    counts = counts.tolist()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        step(spp=spp)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    ms = el * 1e3 / frames
+    rays = counts[0] + counts[1]
+    return {"workload": "configs[3]: Cornell 1920x1080, 256 spp, tiled across %d GPU(s)%s" % (
+                world, " + RCCL HDR all-gather" if world > 1 else ""),
+            "n_gpus": world, "ms_per_frame": round(ms, 3), "Mrays_per_s": round(rays / ms / 1e3, 2),
+            "Msamples_per_s": round(W * H * spp / ms / 1e3, 2), "rays_per_frame": rays}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -436,7 +473,7 @@ def main():
           for _ in range(args.steps)]
     nframe = [0]
 
-    def step(i=None, counters=None):
+    def step(i=None, counters=None, spp=SPP):
         b = nframe[0] % nbuf
         nframe[0] += 1
         if freed[b] is not None:
@@ -447,12 +484,12 @@ def main():
         if interleaved:
             rtamd.check(L.spt_scene_render_groups_async(scene.handle, C.byref(cam), colors[b].data_ptr(),
                                                         seeds0.data_ptr(), seeds.data_ptr(), pixels[b].data_ptr(),
-                                                        W, H, rank, world, 0, SPP, rtamd.SPT_PATH_TRACING, cptr,
+                                                        W, H, rank, world, 0, spp, rtamd.SPT_PATH_TRACING, cptr,
                                                         s.cuda_stream))
         else:
             rtamd.check(L.spt_scene_render_async(scene.handle, C.byref(cam), colors[b].data_ptr(),
                                                  seeds0.data_ptr(), seeds.data_ptr(), pixels[b].data_ptr(), W, H,
-                                                 r0, r1, 0, SPP, rtamd.SPT_PATH_TRACING, cptr, s.cuda_stream))
+                                                 r0, r1, 0, spp, rtamd.SPT_PATH_TRACING, cptr, s.cuda_stream))
         if i is not None:
             ev[i][1].record(s)
         if world > 1:            # RCCL all-gather of the HDR bands + RGBA8 repack
@@ -552,14 +589,15 @@ def main():
                                and torch.equal(ref_p, pixels[last]))], dtype=torch.int32, device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         out["frame_check"] = "assembled frame == single-GPU frame (bit-exact)" if ok.item() else "MISMATCH"
+    if not args.no_whitted and not args.no_cornell_extra:
+        out["configs3"] = configs3_line(step, cnt, dev, world, distributed)
     if rank == 0 and world == 1:
         if not args.no_whitted:
             out["whitted"] = whitted_line(args, dev)
             out["configs4"] = c5_line(args, dev)
             out["queue3203"] = queue_line(args, dev)
-            out["configs2"] = cornell_line(args, dev, 1024, 768, 64, "configs[2]: Cornell 1024x768, 64 spp, 1 GPU")
-            out["configs3_1gpu"] = cornell_line(args, dev, W, H, 256,
-                                                "configs[3] per-GPU work at N=1: Cornell 1920x1080, 256 spp")
+            if not args.no_cornell_extra:
+                out["configs2"] = cornell_line(args, dev, 1024, 768, 64, "configs[2]: Cornell 1024x768, 64 spp, 1 GPU")
             if not args.no_cpu:
                 out["configs0"] = configs0_line(args, dev)
         out["cpu_baseline"] = None if args.no_cpu else cpu_baseline(args)

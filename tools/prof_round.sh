@@ -11,8 +11,8 @@ O=gpurun_out/$R
 mkdir -p $O
 timeout -k 10 300 python3 bench.py > $O/bench.json 2> $O/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o bench \
-    -- python3 bench.py --no-cpu > $O/stats_bench.json 2> $O/stats.err
-B="python3 bench.py --no-cpu --steps 2 --warmup 1"
+    -- python3 bench.py --no-cpu --no-cornell-extra > $O/stats_bench.json 2> $O/stats.err
+B="python3 bench.py --no-cpu --no-cornell-extra --steps 2 --warmup 1"
 i=0
 for set in FETCH_SIZE WRITE_SIZE \
     "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE" \
