@@ -380,13 +380,13 @@ def cornell_line(args, dev, w, h, spp, workload):
             "Msamples_per_s": round(w * h * spp / ms / 1e3, 2), "rays_per_frame": rays}
 
 
-def configs3_line(step, cnt, dev, world, distributed, spp=256, frames=2):
-    """BASELINE configs[3]: the Cornell 1920x1080 frame at 256 spp, tiled
-    across the job's GPUs exactly as the headline steps are (each rank renders
-    its rows, then the RCCL all-gather + repack); a counted frame, then
-    `frames` timed frames bracketed by barrier + synchronize, max over ranks."""
+def tiled_line(step, cnt, dev, world, distributed, workload, spp, frames=2, **scene):
+    """A frame of `workload` tiled across the job's GPUs exactly as the
+    headline steps are (each rank renders its rows, then the RCCL all-gather
+    + repack): a counted frame, then `frames` timed frames bracketed by
+    barrier + synchronize, max over ranks."""
     cnt.zero_()
-    step(counters=cnt, spp=spp)
+    step(counters=cnt, spp=spp, **scene)
     torch.cuda.synchronize(dev)
     counts = cnt.clone()
     if distributed:
@@ -397,7 +397,7 @@ def configs3_line(step, cnt, dev, world, distributed, spp=256, frames=2):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(frames):
-        step(spp=spp)
+        step(spp=spp, **scene)
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
@@ -408,8 +408,7 @@ def configs3_line(step, cnt, dev, world, distributed, spp=256, frames=2):
         el = t.item()
     ms = el * 1e3 / frames
     rays = counts[0] + counts[1]
-    return {"workload": "configs[3]: Cornell 1920x1080, 256 spp, tiled across %d GPU(s)%s" % (
-                world, " + RCCL HDR all-gather" if world > 1 else ""),
+    return {"workload": "%s, tiled across %d GPU(s)%s" % (workload, world, " + RCCL HDR all-gather" if world > 1 else ""),
             "n_gpus": world, "ms_per_frame": round(ms, 3), "Mrays_per_s": round(rays / ms / 1e3, 2),
             "Msamples_per_s": round(W * H * spp / ms / 1e3, 2), "rays_per_frame": rays}
 
@@ -473,7 +472,9 @@ def main():
           for _ in range(args.steps)]
     nframe = [0]
 
-    def step(i=None, counters=None, spp=SPP):
+    def step(i=None, counters=None, spp=SPP, sc=None, cm=None):
+        sc = scene if sc is None else sc
+        cm = cam if cm is None else cm
         b = nframe[0] % nbuf
         nframe[0] += 1
         if freed[b] is not None:
@@ -482,12 +483,12 @@ def main():
             ev[i][0].record(s)
         cptr = counters.data_ptr() if counters is not None else None
         if interleaved:
-            rtamd.check(L.spt_scene_render_groups_async(scene.handle, C.byref(cam), colors[b].data_ptr(),
+            rtamd.check(L.spt_scene_render_groups_async(sc.handle, C.byref(cm), colors[b].data_ptr(),
                                                         seeds0.data_ptr(), seeds.data_ptr(), pixels[b].data_ptr(),
                                                         W, H, rank, world, 0, spp, rtamd.SPT_PATH_TRACING, cptr,
                                                         s.cuda_stream))
         else:
-            rtamd.check(L.spt_scene_render_async(scene.handle, C.byref(cam), colors[b].data_ptr(),
+            rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cm), colors[b].data_ptr(),
                                                  seeds0.data_ptr(), seeds.data_ptr(), pixels[b].data_ptr(), W, H,
                                                  r0, r1, 0, spp, rtamd.SPT_PATH_TRACING, cptr, s.cuda_stream))
         if i is not None:
@@ -590,7 +591,14 @@ def main():
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         out["frame_check"] = "assembled frame == single-GPU frame (bit-exact)" if ok.item() else "MISMATCH"
     if not args.no_whitted and not args.no_cornell_extra:
-        out["configs3"] = configs3_line(step, cnt, dev, world, distributed)
+        out["configs3"] = tiled_line(step, cnt, dev, world, distributed, "configs[3]: Cornell 1920x1080, 256 spp", 256)
+    if not args.no_whitted:
+        c4s, c4n, c4cam = rtamd.scenes.complex10k()
+        rtamd.scenes.update_camera(c4cam, W, H)
+        c4scene = rtamd.SmallptScene(c4s, c4n)
+        out["configs4_tiled"] = tiled_line(step, cnt, dev, world, distributed,
+                                           "configs[4]: 10k-sphere scene_build_complex, 1920x1080, 64 spp", SPP,
+                                           sc=c4scene, cm=c4cam)
     if rank == 0 and world == 1:
         if not args.no_whitted:
             out["whitted"] = whitted_line(args, dev)
