@@ -621,7 +621,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
               float *__restrict__ colors, const uint32_t *seeds_in,
               uint32_t *seeds_out, uint32_t *__restrict__ pixels, int w, int h,
               int row_begin, int row_end, int tiles_x, int ntiles, int gstride, int first_sample, int nsamples,
-              int prio_late,
+              int prio_sched,
               const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
               const float4 *__restrict__ g_col, const float4 *__restrict__ g_lrec, int nlights,
               BvhView bvh, unsigned long long *__restrict__ counters)
@@ -708,10 +708,9 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         bool walking = false;  //   and whether it is suspended mid-walk
         constexpr float nc = 1.f, nt = 1.5f;
 #if RT_SPT_PRIO
-        // Levels at 1/4, 1/2, 3/4 of the samples; prio_late (windows of <= 8
-        // waves per SIMD, one or two rounds of 16-wave blocks): at 1/2, 3/4,
-        // 7/8 -- finer where the co-resident waves drain.
-        int prio_level = 0, prio_next = prio_late ? nsamples / 2 : nsamples / 4;
+        // prio_sched: the three level boundaries as fractions of the samples
+        // (8 bits each, in 1/256; host: prio_schedule).
+        int prio_level = 0, prio_next = (nsamples * (prio_sched & 255)) >> 8;
         __builtin_amdgcn_s_setprio(3);
 #endif
         while (true) {
@@ -767,7 +766,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             // together.  (s_setprio only reorders issue; results unchanged.)
             if (!wave_any(k < prio_next)) {
                 prio_level++;
-                prio_next = prio_late ? nsamples - (nsamples >> (prio_level + 1)) : (prio_level + 1) * nsamples / 4;
+                prio_next = prio_level < 3 ? (nsamples * ((prio_sched >> (8 * prio_level)) & 255)) >> 8 : nsamples;
                 if (prio_level == 1) __builtin_amdgcn_s_setprio(2);
                 else if (prio_level == 2) __builtin_amdgcn_s_setprio(1);
                 else __builtin_amdgcn_s_setprio(0);
@@ -1095,6 +1094,7 @@ __global__ void __launch_bounds__(256) pack_kernel(const float *__restrict__ col
 
 // ------------------------------------------------------------------ host side
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
@@ -1146,13 +1146,17 @@ Shape launch_shape(const spt_scene &sc, int w, int r0, int r1, int gstride = 1)
     return g;
 }
 
-// Priority levelling schedule (render_kernel's prio_late): the late form
-// for the 16-wave block shape (multi-GPU windows); RT_SPT_PRIO_LATE=0/1
-// forces it (A/B).
-int prio_late(const Shape &g)
+// Priority levelling schedule (render_kernel's prio_sched): levels at 1/4,
+// 1/2, 3/4 of the samples for the full-frame shape; for the 16-wave block
+// shape (multi-GPU windows of <= 8 waves per SIMD, one or two rounds) at
+// 1/2, 3/4, 7/8 -- finer where the co-resident waves drain.
+// RT_SPT_PRIO_SCHED=a,b,c (in 1/256) overrides it (A/B).
+int prio_schedule(const Shape &g)
 {
-    if (const char *e = getenv("RT_SPT_PRIO_LATE")) return atoi(e) != 0;
-    return g.wpb == 16;
+    int a = 64, b = 128, c = 192;
+    if (g.wpb == 16) { a = 128; b = 192; c = 224; }
+    if (const char *e = getenv("RT_SPT_PRIO_SCHED")) sscanf(e, "%d,%d,%d", &a, &b, &c);
+    return (a & 255) | ((b & 255) << 8) | ((c & 255) << 16);
 }
 
 template <bool DL, bool COUNT, int GEO, bool DUAL = false>
@@ -1167,7 +1171,7 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     if (g.wpb == 16 && lds < 81 * 1024) lds = 81 * 1024;   // > half the CU's 160 KiB: one block per CU
     hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.gstride, first,
-                       ns, prio_late(g), gg, ge, gc, gl, sc.nlights, sc.bvh, cnt);
+                       ns, prio_schedule(g), gg, ge, gc, gl, sc.nlights, sc.bvh, cnt);
 }
 
 template <int GEO>
