@@ -621,7 +621,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
               float *__restrict__ colors, const uint32_t *seeds_in,
               uint32_t *seeds_out, uint32_t *__restrict__ pixels, int w, int h,
               int row_begin, int row_end, int tiles_x, int ntiles, int gstride, int first_sample, int nsamples,
-              int prio_sched,
+              int prio_sched, const int *__restrict__ group_order, unsigned *__restrict__ group_cost,
               const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
               const float4 *__restrict__ g_col, const float4 *__restrict__ g_lrec, int nlights,
               BvhView bvh, unsigned long long *__restrict__ counters)
@@ -653,7 +653,13 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // j * gridDim.x + b, so the groups of a 16-wave block sample the whole
     // window (per-CU work evens out when one block fills a CU).
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int tile = ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) * 4 + (wave & 3);
+    // group_order (optional): dispatch slot -> group, heaviest groups of the
+    // previous launch first (host: adaptive schedule); results do not depend
+    // on it.
+    const int slot = (wave >> 2) * (int)gridDim.x + (int)blockIdx.x;
+    const int grp = group_order ? group_order[slot] : slot;
+    const int tile = grp * 4 + (wave & 3);
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     const int x = (tile % tiles_x) * 8 + (lane & 7);
     // gstride > 1: the window is every gstride-th 8-row group from row_begin
     // (spt_scene_render_groups_async, multi-GPU load balance).
@@ -1046,6 +1052,8 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         seeds_out[2 * (size_t)i] = s0;
         seeds_out[2 * (size_t)i + 1] = s1;
     }
+    if (group_cost && lane == 0)        // this wave's duration (100 MHz ticks), summed per group
+        atomicAdd(&group_cost[grp], (unsigned)(__builtin_amdgcn_s_memrealtime() - t_start));
     if (COUNT) {
         const unsigned long long c[4] = {cnt.isect, cnt.isectp, cnt.tests, cnt.samples};
         flush_counters<4>(counters, c);
@@ -1104,6 +1112,23 @@ __global__ void __launch_bounds__(256) pack_kernel(const float *__restrict__ col
 
 // A prepared scene (spt_scene_create): device AoS copy for the per-block LDS
 // staging, device SoA + light list for scenes above the LDS budget.
+// Adaptive dispatch order of a scene's tile groups (scene_render): the first
+// launch for a given window / camera / sample count records each group's
+// wave time; once that is back on the host, later launches of the same key
+// dispatch the groups heaviest first, so the long tiles of a non-uniform
+// scene (configs[4]: per-wave work varies 6x) start at once instead of
+// setting the frame's tail.  Scheduling only: every pixel's computation is
+// unchanged.
+struct SptSched {
+    int w = 0, h = 0, r0 = 0, r1 = 0, gstride = 0, ns = -1, mode = -1, nslots = 0;
+    rt_camera cam = {};
+    int state = 0;                    // 0: none, 1: costs recorded (copy in flight), 2: order set
+    int cap = 0;
+    unsigned *d_cost = nullptr, *h_cost = nullptr;   // h_*: pinned
+    int *d_order = nullptr, *h_order = nullptr;
+    hipEvent_t ev = nullptr;
+};
+
 struct spt_scene {
     int device = -1;
     int cus = 256;
@@ -1115,6 +1140,7 @@ struct spt_scene {
     rt::smallpt::BvhView bvh = {};
     std::vector<rt_sphere> host;
     bool force_global = false;        // RT_SPT_GEO=global: scalar-load path at any size (A/B)
+    mutable SptSched sched;           // adaptive group order (hierarchy scenes)
 };
 
 namespace {
@@ -1124,7 +1150,11 @@ namespace {
 // four tiles per SIMD (a multi-GPU row band): then 1024-thread blocks with
 // more than half the CU's LDS reserved, so a CU holds exactly one and every
 // SIMD gets four waves, instead of the dispatcher's uneven 3..5 per SIMD.
-struct Shape { int tiles_x, ntiles, gstride, wpb, nblocks; };
+struct Shape {
+    int tiles_x, ntiles, gstride, wpb, nblocks;
+    const int *order = nullptr;       // adaptive schedule (render_kernel's group_order / group_cost)
+    unsigned *cost = nullptr;
+};
 // Rows [r0, r1), or (gstride > 1) the 8-row groups r0/8, r0/8 + gstride, ...
 // below r1 (r0 a multiple of 8).
 Shape launch_shape(const spt_scene &sc, int w, int r0, int r1, int gstride = 1)
@@ -1171,7 +1201,7 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     if (g.wpb == 16 && lds < 81 * 1024) lds = 81 * 1024;   // > half the CU's 160 KiB: one block per CU
     hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.gstride, first,
-                       ns, prio_schedule(g), gg, ge, gc, gl, sc.nlights, sc.bvh, cnt);
+                       ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt);
 }
 
 template <int GEO>
@@ -1482,18 +1512,95 @@ extern "C" int spt_scene_destroy(spt_scene *sc)
     if (sc->d_spheres) (void)hipFree(sc->d_spheres);
     if (sc->d_soa) (void)hipFree(sc->d_soa);
     if (sc->d_bvh) (void)hipFree(sc->d_bvh);
+    SptSched &q = sc->sched;
+    if (q.d_cost) (void)hipFree(q.d_cost);
+    if (q.d_order) (void)hipFree(q.d_order);
+    if (q.h_cost) (void)hipHostFree(q.h_cost);
+    if (q.h_order) (void)hipHostFree(q.h_order);
+    if (q.ev) (void)hipEventDestroy(q.ev);
     delete sc;
     return RT_OK;
 }
 
 namespace {
+// Adaptive order (SptSched) for one launch: sets g.order / g.cost; returns
+// true if the caller must queue the cost read-back after the launch.
+bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, int r0, int r1, int gstride,
+                  int ns, int mode, const rt_camera &cam)
+{
+    const char *e = getenv("RT_SPT_SCHED");
+    if (!(e ? atoi(e) != 0 : sc.bvh.node != nullptr)) return false;
+    SptSched &q = sc.sched;
+    const int nslots = g.nblocks * (g.wpb / 4);
+    if (!(q.w == w && q.h == h && q.r0 == r0 && q.r1 == r1 && q.gstride == gstride && q.ns == ns &&
+          q.mode == mode && q.nslots == nslots && memcmp(&q.cam, &cam, sizeof(cam)) == 0)) {
+        q.w = w; q.h = h; q.r0 = r0; q.r1 = r1; q.gstride = gstride; q.ns = ns; q.mode = mode;
+        q.nslots = nslots; q.cam = cam;
+        q.state = 0;
+    }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        if (q.state == 2) g.order = q.d_order;         // a device pointer: capture-safe
+        return false;
+    }
+    if (nslots > q.cap) {                               // grow (the old buffers may still be read)
+        if (q.ev && hipEventSynchronize(q.ev) != hipSuccess) return false;
+        if (hipStreamSynchronize(s) != hipSuccess) return false;
+        if (q.d_cost) (void)hipFree(q.d_cost);
+        if (q.d_order) (void)hipFree(q.d_order);
+        if (q.h_cost) (void)hipHostFree(q.h_cost);
+        if (q.h_order) (void)hipHostFree(q.h_order);
+        q.d_cost = q.h_cost = nullptr;
+        q.d_order = q.h_order = nullptr;
+        q.cap = 0;
+        if (hipMalloc(&q.d_cost, sizeof(unsigned) * nslots) != hipSuccess ||
+            hipMalloc(&q.d_order, sizeof(int) * nslots) != hipSuccess ||
+            hipHostMalloc(&q.h_cost, sizeof(unsigned) * nslots) != hipSuccess ||
+            hipHostMalloc(&q.h_order, sizeof(int) * nslots) != hipSuccess)
+            return false;                               // plain launches (the frees above are safe)
+        if (!q.ev && hipEventCreateWithFlags(&q.ev, hipEventDisableTiming) != hipSuccess) return false;
+        q.cap = nslots;
+        q.state = 0;
+    }
+    if (q.state == 1 && hipEventQuery(q.ev) == hipSuccess) {
+        // heaviest first; ties (and the groups past the window: no tiles, 0)
+        // in slot order
+        std::vector<int> idx(nslots);
+        for (int i = 0; i < nslots; i++) idx[i] = i;
+        std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return q.h_cost[a] > q.h_cost[b]; });
+        memcpy(q.h_order, idx.data(), sizeof(int) * nslots);
+        if (hipMemcpyAsync(q.d_order, q.h_order, sizeof(int) * nslots, hipMemcpyHostToDevice, s) != hipSuccess)
+            return false;
+        q.state = 2;
+    }
+    if (q.state == 2) {
+        g.order = q.d_order;
+        return false;
+    }
+    if (q.state == 0) {
+        if (hipMemsetAsync(q.d_cost, 0, sizeof(unsigned) * nslots, s) != hipSuccess) return false;
+        g.cost = q.d_cost;
+        return true;
+    }
+    return false;                                       // state 1, read-back in flight: plain launch
+}
+
+void sched_after(const spt_scene &sc, hipStream_t s)
+{
+    SptSched &q = sc.sched;
+    if (hipMemcpyAsync(q.h_cost, q.d_cost, sizeof(unsigned) * q.nslots, hipMemcpyDeviceToHost, s) == hipSuccess &&
+        hipEventRecord(q.ev, s) == hipSuccess)
+        q.state = 1;
+}
+
 int scene_render(const spt_scene *sc, const rt_camera *camera, float *d_colors, const uint32_t *d_seeds_in,
                  uint32_t *d_seeds_out, uint32_t *d_pixels, int w, int h, int row_begin, int row_end, int gstride,
                  int first_sample, int nsamples, int mode, uint64_t *d_counters, void *stream)
 {
     if (row_begin >= row_end) return RT_OK;
-    const Shape grid = launch_shape(*sc, w, row_begin, row_end, gstride);
+    Shape grid = launch_shape(*sc, w, row_begin, row_end, gstride);
     hipStream_t s = (hipStream_t)stream;
+    const bool record = sched_before(*sc, grid, s, w, h, row_begin, row_end, gstride, nsamples, mode, *camera);
     unsigned long long *cnt = (unsigned long long *)d_counters;
     const bool dl = mode == SPT_DIRECT_LIGHTING;
     if (sc->bvh.node)
@@ -1507,7 +1614,9 @@ int scene_render(const spt_scene *sc, const rt_camera *camera, float *d_colors, 
     else
         launch_mode<rt::smallpt::GEO_GLOBAL>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
                               d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
-    return rtrt::check_launch("spt render_kernel");
+    const int rc = rtrt::check_launch("spt render_kernel");
+    if (rc == RT_OK && record) sched_after(*sc, s);
+    return rc;
 }
 }  // namespace
 

@@ -220,6 +220,46 @@ def test_scene_cache_follows_the_array(rt, oracle):
         assert (f.colors.view(np.uint32) == ref_col.view(np.uint32)).all() and (f.pixels == ref_px).all()
 
 
+@pytest.mark.parametrize("sched", ["0", "1"])
+def test_adaptive_group_order_is_exact(rt, monkeypatch, sched):
+    """Hierarchy scenes dispatch their tile groups heaviest-first once a
+    launch has recorded the groups' wave times (SptSched): the 1st launch of a
+    key records, the 2nd builds the order, the 3rd and later use it.  Every
+    launch must give the same bits as the plain dispatch (RT_SPT_SCHED=0),
+    counted and uncounted, full frame and a row window."""
+    import ctypes as C
+    import torch
+    monkeypatch.setenv("RT_SPT_SCHED", sched)
+    w, h = 480, 270
+    spheres, n, cam = rt.scenes.complex10k()
+    rt.scenes.update_camera(cam, w, h)
+    sc = rt.SmallptScene(spheres, n)
+    dev = torch.device("cuda", 0)
+    seeds0 = torch.from_numpy(rt.scenes.seeds(w, h).view(np.int32)).to(dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    outs = []
+    for r0, r1 in ((0, h), (0, h), (0, h), (0, h), (40, 200), (40, 200), (40, 200)):
+        for counted in (False, True):
+            col = torch.zeros(3 * w * h, dtype=torch.float32, device=dev)
+            seeds = torch.zeros_like(seeds0)
+            px = torch.zeros(w * h, dtype=torch.int32, device=dev)
+            cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+            rt.check(rt.lib().spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                                     seeds.data_ptr(), px.data_ptr(), w, h, r0, r1, 0, 3, 0,
+                                                     cnt.data_ptr() if counted else None, st))
+            torch.cuda.synchronize()
+            outs.append(((r0, r1), col.cpu().numpy().view(np.uint32), seeds.cpu().numpy(), px.cpu().numpy(),
+                         cnt.cpu().numpy() if counted else None))
+    ref = {}
+    for key, c, s_, p, k in outs:
+        if key not in ref:
+            ref[key] = (c, s_, p)
+        rc, rs, rp = ref[key]
+        assert (c == rc).all() and (s_ == rs).all() and (p == rp).all(), key
+    full = [k for key, *_, k in outs if key == (0, h) and k is not None]
+    assert all((k == full[0]).all() for k in full)
+
+
 def _bvh_vs_scan(rt, monkeypatch, spheres, n, cam, w, h, spp, mode=0):
     """Renders with the hierarchy and with the full scan (RT_SPT_NO_BVH),
     each with and without the work counters (the uncounted kernels stop a

@@ -25,9 +25,16 @@ st = torch.cuda.current_stream(dev)
 L = rtamd.lib()
 
 
+R0, R1 = 0, H
+if os.environ.get("BAND"):                          # BAND=k/N: row band k of N (per-GPU work at N GPUs)
+    from rtamd import dist as rdist
+    k, N = (int(v) for v in os.environ["BAND"].split("/"))
+    R0, R1 = rdist.row_band(k, N, H)
+
+
 def run(c=None):
     rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
-                                         seeds.data_ptr(), px.data_ptr(), W, H, 0, H, 0, SPP, 0,
+                                         seeds.data_ptr(), px.data_ptr(), W, H, R0, R1, 0, SPP, 0,
                                          c.data_ptr() if c is not None else None, st.cuda_stream))
 
 
@@ -61,8 +68,8 @@ for _ in range(int(os.environ.get("REPS", "1"))):
     torch.cuda.synchronize()
     ts.append(a.elapsed_time(b))
 ms = float(np.median(ts))
-print("c5 %dx%d spp=%d spheres=%d: %.2f ms (median of %d, min %.2f), rays %d, %.1f Mrays/s, sphere tests %d" % (
-    W, H, SPP, n, ms, len(ts), min(ts), rays, rays / ms / 1e3, int(cnt[2])))
+print("c5 %dx%d rows [%d,%d) spp=%d spheres=%d: %.2f ms (median of %d, min %.2f), rays %d, %.1f Mrays/s, sphere tests %d" % (
+    W, H, R0, R1, SPP, n, ms, len(ts), min(ts), rays, rays / ms / 1e3, int(cnt[2])))
 if int(cnt[7]):
     q = rays
     print("  per query: %.1f nodes, %.1f sphere tests; lane trips / (64 x wave trips) = %.3f" % (

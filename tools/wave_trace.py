@@ -66,6 +66,14 @@ def analyse(tag, t, gx, gy, save=None):
           % (it.mean(), it.std() / it.mean(), it.min(), it.max(), (mx[live] * 64 / it).mean()))
     print("   wave duration ms: mean %.3f min %.3f max %.3f" % ((e - s)[live].mean(), (e - s)[live].min(),
                                                              (e - s)[live].max()))
+    dur = (e - s)
+    idx = np.argsort(-dur)[:8]
+    wid = np.nonzero(t[:, 1] != 0)[0] if False else None
+    print("   longest waves (start ms, duration ms, sum lane iters): %s" % ", ".join(
+        "(%.2f, %.2f, %d)" % (s[i], dur[i], iters[i]) for i in idx))
+    late = s > 0.5 * span
+    print("   waves starting after half the span: %d, their mean duration %.3f ms (all: %.3f)"
+          % (late.sum(), dur[late].mean() if late.any() else 0.0, dur.mean()))
     if save:
         os.makedirs(save, exist_ok=True)
         np.save(os.path.join(save, tag + ".npy"), t)
@@ -78,8 +86,12 @@ def main():
     dev = torch.device("cuda", 0)
     L = rtamd.lib()
     L.spt_trace_set.argtypes = [C.c_void_p]
-    S, n = rtamd.scenes.cornell()
-    cam = rtamd.scenes.cornell_camera(W, H)
+    if os.environ.get("SCENE") == "c4":            # BASELINE configs[4] (hierarchy kernel)
+        S, n, cam = rtamd.scenes.complex10k()
+        rtamd.scenes.update_camera(cam, W, H)
+    else:
+        S, n = rtamd.scenes.cornell()
+        cam = rtamd.scenes.cornell_camera(W, H)
     sc = rtamd.SmallptScene(S, n)
     seeds0 = torch.from_numpy(rtamd.scenes.seeds(W, H).view(np.int32)).to(dev)
     seeds = torch.empty_like(seeds0)
@@ -87,7 +99,7 @@ def main():
     px = torch.zeros(W * H, dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev)
     run(L, sc, cam, seeds0, seeds, col, px, 0, H, st)          # warm-up
-    for N in (1, 2, 4, 8):
+    for N in [int(v) for v in os.environ.get("NS", "1,2,4,8").split(",")]:
         r0, r1 = rdist.row_band(0 if N == 1 else N // 2, N, H)
         t, gx, gy = run(L, sc, cam, seeds0, seeds, col, px, r0, r1, st)
         analyse("N%d" % N, t, gx, gy, save)
