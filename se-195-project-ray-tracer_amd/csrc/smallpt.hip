@@ -716,8 +716,15 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
 #if RT_SPT_PRIO
         // prio_sched: the three level boundaries as fractions of the samples
         // (8 bits each, in 1/256; host: prio_schedule).
-        int prio_level = 0, prio_next = (nsamples * (prio_sched & 255)) >> 8;
-        __builtin_amdgcn_s_setprio(3);
+        // With an adaptive order, the first (prio_sched >> 24) * 16 group
+        // slots hold the heaviest groups: their waves keep the top priority
+        // throughout (they set the frame's critical path); the others level
+        // down from 2.
+        const bool heavy = slot < ((prio_sched >> 24) & 255) * 16;
+        const bool top3 = heavy || (prio_sched >> 24) == 0;
+        int prio_level = 0, prio_next = heavy ? nsamples + 1 : (nsamples * (prio_sched & 255)) >> 8;
+        if (top3) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(2);
 #endif
         while (true) {
             // ---- pass B: DIFF bounce (geomfunc.h:229-269) or camera ray
@@ -773,8 +780,8 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             if (!wave_any(k < prio_next)) {
                 prio_level++;
                 prio_next = prio_level < 3 ? (nsamples * ((prio_sched >> (8 * prio_level)) & 255)) >> 8 : nsamples;
-                if (prio_level == 1) __builtin_amdgcn_s_setprio(2);
-                else if (prio_level == 2) __builtin_amdgcn_s_setprio(1);
+                if (prio_level == 1 && top3) __builtin_amdgcn_s_setprio(2);
+                else if ((prio_level == 2 && top3) || (prio_level == 1 && !top3)) __builtin_amdgcn_s_setprio(1);
                 else __builtin_amdgcn_s_setprio(0);
             }
 #endif
@@ -1154,6 +1161,7 @@ struct Shape {
     int tiles_x, ntiles, gstride, wpb, nblocks;
     const int *order = nullptr;       // adaptive schedule (render_kernel's group_order / group_cost)
     unsigned *cost = nullptr;
+    int heavy16 = 0;                  // with order: heaviest slots kept at top priority, in 16s
 };
 // Rows [r0, r1), or (gstride > 1) the 8-row groups r0/8, r0/8 + gstride, ...
 // below r1 (r0 a multiple of 8).
@@ -1186,7 +1194,7 @@ int prio_schedule(const Shape &g)
     int a = 64, b = 128, c = 192;
     if (g.wpb == 16) { a = 128; b = 192; c = 224; }
     if (const char *e = getenv("RT_SPT_PRIO_SCHED")) sscanf(e, "%d,%d,%d", &a, &b, &c);
-    return (a & 255) | ((b & 255) << 8) | ((c & 255) << 16);
+    return (a & 255) | ((b & 255) << 8) | ((c & 255) << 16) | ((g.order ? g.heavy16 & 255 : 0) << 24);
 }
 
 template <bool DL, bool COUNT, int GEO, bool DUAL = false>
@@ -1575,6 +1583,11 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
     }
     if (q.state == 2) {
         g.order = q.d_order;
+        int heavy = sc.cus / 4;                         // a heavy group (a wave per SIMD) on every 4th CU
+                                                        // (measured: 0, cus/4, cus/2, cus, 4cus groups: 32.6,
+                                                        // 31.8, 32.2, 33.2, 32.6 ms, configs[4])
+        if (const char *he = getenv("RT_SPT_HEAVY")) heavy = atoi(he);
+        g.heavy16 = std::min(std::max((heavy + 15) / 16, 0), 255);
         return false;
     }
     if (q.state == 0) {
