@@ -158,8 +158,15 @@ int spt_render_async(const rt_sphere *d_spheres, unsigned nspheres, const rt_cam
 typedef struct spt_scene spt_scene;
 int spt_scene_create(const rt_sphere *spheres, unsigned nspheres, spt_scene **out);
 int spt_scene_destroy(spt_scene *scene);
-/* spt_render_async on a prepared scene: no host<->device traffic, fully
- * asynchronous on `stream` (graph-capturable). */
+/* spt_render_async on a prepared scene: asynchronous on `stream`
+ * (graph-capturable).  Hierarchy scenes (>= 256 spheres) learn a dispatch
+ * order: the first launch of a (window, camera, nsamples, mode) key records
+ * each tile group's wave time and queues a 32-KB-class read-back of it; once
+ * that has landed, launches of the key dispatch the heaviest groups first
+ * (one small upload).  Scheduling only -- results are identical; during
+ * stream capture the learnt order is used but not updated.  A scene's order
+ * is updated by the calling thread: render one scene from one host thread
+ * at a time. */
 int spt_scene_render_async(const spt_scene *scene, const rt_camera *camera, float *d_colors,
                            const uint32_t *d_seeds_in, uint32_t *d_seeds_out, uint32_t *d_pixels,
                            int w, int h, int row_begin, int row_end, int first_sample, int nsamples,
