@@ -782,6 +782,8 @@ fix_kernel(QArgs A, float DX, float DY, uint32_t *__restrict__ out, unsigned lon
         }
         if (__builtin_amdgcn_ballot_w64(over) != 0 && threadIdx.x == 0) *(volatile int *)A.ovf = 1;
     }
+    // blocks past the work (a handful of flagged pixels) leave before staging the scene
+    if ((int)blockIdx.x * 64 >= (nfix > A.fixcap ? (A.npix + 31) >> 5 : nfix)) return;
     __shared__ Scene S;
     __shared__ int ring[RING][64];
     load_scene(S, A.scene);

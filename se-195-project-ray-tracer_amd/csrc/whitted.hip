@@ -790,10 +790,9 @@ __global__ void __launch_bounds__(64)
 fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict__ sy_tab, float DX, float DY,
              unsigned long long *__restrict__ counters)
 {
-    __shared__ Scene S;
-    load_scene(S, A.scene);
     const int nfix = CNT(A, C_FIX);
-    if (blockIdx.x == 0 && nfix > 0) {
+    if (nfix == 0) return;
+    if (blockIdx.x == 0) {
         // Tell the host when a queue asked for more than its pages (a segment
         // counter past its limit) or a TIR list for more than its capacity:
         // the next frame gets a larger pool.
@@ -805,6 +804,10 @@ fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict
         }
         if (__builtin_amdgcn_ballot_w64(over) != 0 && lane == 0) *(volatile int *)A.ovf = 1;
     }
+    // blocks past the work leave before staging the scene
+    if ((int)(blockIdx.x * blockDim.x) >= (nfix > A.fixcap ? (A.ntrees + 31) >> 5 : nfix)) return;
+    __shared__ Scene S;
+    load_scene(S, A.scene);
     const bool scan = nfix > A.fixcap;                  // the list overflowed: walk the bitmask
     const int nitems = scan ? (A.ntrees + 31) >> 5 : nfix;
     Counts cnt = {0, 0, 0, 0};
