@@ -32,10 +32,20 @@ if os.environ.get("BAND"):                          # BAND=k/N: row band k of N 
     R0, R1 = rdist.row_band(k, N, H)
 
 
+GROUP = os.environ.get("GROUP")                    # GROUP=k/N: interleaved 8-row groups of rank k of N
+
+
 def run(c=None):
-    rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
-                                         seeds.data_ptr(), px.data_ptr(), W, H, R0, R1, 0, SPP, 0,
-                                         c.data_ptr() if c is not None else None, st.cuda_stream))
+    cp = c.data_ptr() if c is not None else None
+    if GROUP:
+        k, N = (int(v) for v in GROUP.split("/"))
+        rtamd.check(L.spt_scene_render_groups_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                                    seeds.data_ptr(), px.data_ptr(), W, H, k, N, 0, SPP, 0, cp,
+                                                    st.cuda_stream))
+    else:
+        rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                             seeds.data_ptr(), px.data_ptr(), W, H, R0, R1, 0, SPP, 0, cp,
+                                             st.cuda_stream))
 
 
 stats = getattr(L, "spt_bvh_stats_read", None)   # RT_BVH_STATS builds only
