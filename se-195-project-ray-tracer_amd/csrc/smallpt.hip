@@ -656,10 +656,15 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // group_order (optional): dispatch slot -> group, heaviest groups of the
     // previous launch first (host: adaptive schedule); results do not depend
     // on it.
+    // Compiled into the hierarchy kernels only: in the full-scan kernels
+    // (Cornell) the order/cost plumbing cost 1.4 % of the frame and 8 % of an
+    // N = 8 band (measured A/B) although it is never used there.
+    constexpr bool SCHED = GEO == GEO_BVH;
     const int slot = (wave >> 2) * (int)gridDim.x + (int)blockIdx.x;
-    const int grp = group_order ? group_order[slot] : slot;
+    const int grp = (SCHED && group_order) ? group_order[slot] : slot;
     const int tile = grp * 4 + (wave & 3);
-    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_start = 0;
+    if (SCHED) t_start = __builtin_amdgcn_s_memrealtime();
     const int x = (tile % tiles_x) * 8 + (lane & 7);
     // gstride > 1: the window is every gstride-th 8-row group from row_begin
     // (spt_scene_render_groups_async, multi-GPU load balance).
@@ -720,8 +725,8 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         // slots hold the heaviest groups: their waves keep the top priority
         // throughout (they set the frame's critical path); the others level
         // down from 2.
-        const bool heavy = slot < ((prio_sched >> 24) & 255) * 16;
-        const bool top3 = heavy || (prio_sched >> 24) == 0;
+        const bool heavy = SCHED && slot < ((prio_sched >> 24) & 255) * 16;
+        const bool top3 = !SCHED || heavy || (prio_sched >> 24) == 0;
         int prio_level = 0, prio_next = heavy ? nsamples + 1 : (nsamples * (prio_sched & 255)) >> 8;
         if (top3) __builtin_amdgcn_s_setprio(3);
         else __builtin_amdgcn_s_setprio(2);
@@ -1059,7 +1064,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         seeds_out[2 * (size_t)i] = s0;
         seeds_out[2 * (size_t)i + 1] = s1;
     }
-    if (group_cost && lane == 0)        // this wave's duration (100 MHz ticks), summed per group
+    if (SCHED && group_cost && lane == 0)   // this wave's duration (100 MHz ticks), summed per group
         atomicAdd(&group_cost[grp], (unsigned)(__builtin_amdgcn_s_memrealtime() - t_start));
     if (COUNT) {
         const unsigned long long c[4] = {cnt.isect, cnt.isectp, cnt.tests, cnt.samples};
@@ -1537,7 +1542,7 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
                   int ns, int mode, const rt_camera &cam)
 {
     const char *e = getenv("RT_SPT_SCHED");
-    if (!(e ? atoi(e) != 0 : sc.bvh.node != nullptr)) return false;
+    if (!sc.bvh.node || (e && atoi(e) == 0)) return false;   // the full-scan kernels have no order/cost code
     SptSched &q = sc.sched;
     const int nslots = g.nblocks * (g.wpb / 4);
     if (!(q.w == w && q.h == h && q.r0 == r0 && q.r1 == r1 && q.gstride == gstride && q.ns == ns &&
