@@ -1017,8 +1017,14 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 }
             };
             if (a_L || a_R) pass_a(true);
-            while (wave_any(a_L)) {
-                if (a_L) pass_a(false);
+            // With one light the pass above always leaves a_L false (lit, or
+            // li = 1 = nlights); the scalar test keeps the light-only loop --
+            // and the copies of the loop-carried state the compiler puts at
+            // its header, 12 VALU ops per iteration -- out of such scenes.
+            if (S.nlights > 1) {
+                while (wave_any(a_L)) {
+                    if (a_L) pass_a(false);
+                }
             }
             if (was_R) done = depth > 6;
             if (lights_done) {                                  // :229-230, then the bounce
