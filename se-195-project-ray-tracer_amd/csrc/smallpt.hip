@@ -766,10 +766,10 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     rorig = vadd(rorig, mk(cam.orig.x, cam.orig.y, cam.orig.z));
                     ray.o = rorig;
                     ray.d = vn;
-                    rad = mk(0.f, 0.f, 0.f);
-                    thr = mk(1.f, 1.f, 1.f);
-                    depth = 0;
-                    specular = true;
+                    // (rad, thr, depth, specular were reset when the previous
+                    // sample finished: writing them only on this side made the
+                    // compiler copy all six accumulators out and back around
+                    // the branch every pass)
                 }
                 need_bounce = need_cam = false;
             }
@@ -1058,6 +1058,10 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 k++;
                 need_cam = k < nsamples;
                 fin = false;
+                rad = mk(0.f, 0.f, 0.f);                        // the next sample's path state
+                thr = mk(1.f, 1.f, 1.f);                        // (smallptCPU.cpp:89-105 via pass B)
+                depth = 0;
+                specular = true;
             }
         }
         if (nsamples > 0) {
