@@ -636,7 +636,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     Scene S;
     if (LDS) {
         float4 *s = (float4 *)smem;
-        const int nrec = 3 * nspheres + 3 * nlights;
+        const int nrec = 3 * nspheres + 3 * (nlights > 0 ? nlights : 1);   // a light-free scene: one zero record
         for (int i = threadIdx.x; i < nrec; i += blockDim.x) s[i] = g_geo[i];
         __syncthreads();
         S.geo = s; S.emi = s + nspheres; S.col = s + 2 * nspheres; S.lrec = s + 3 * nspheres;
@@ -922,11 +922,13 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             const auto pass_a = [&](const bool with_r) {
                 {
                     SPT_PROF(PB_LIGHT);
-                    float4 lg = make_float4(0.f, 0.f, 0.f, 0.f), lc = lg;
-                    if (a_L) {
-                        lg = S.lrec[3 * li];                    // centre
-                        lc = S.lrec[3 * li + 1];                // colour.xyz, rad
-                    }
+                    // Loaded by every lane (an R-only lane's light terms are
+                    // discarded by the selects below; li is clamped into the
+                    // light list) -- a conditional load left five zeroing
+                    // moves and a branch in every pass.
+                    const int lj = li < S.nlights ? li : 0;
+                    const float4 lg = S.lrec[3 * lj];           // centre
+                    const float4 lc = S.lrec[3 * lj + 1];       // colour.xyz, rad
                     // REFR terms (:281-296), rebuilt here from the few values
                     // kept since the hit: normal = inv_sign * nl exactly
                     // (inv_sign = +-1), and, rounding being sign-symmetric,
@@ -1220,7 +1222,7 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     constexpr bool LDS = GEO == rt::smallpt::GEO_LDS;
     const int n = sc.n;
     const float4 *gg = sc.d_soa, *ge = gg + n, *gc = ge + n, *gl = gc + n;
-    size_t lds = LDS ? (size_t)(3 * n + 3 * sc.nlights) * sizeof(float4) : 0;
+    size_t lds = LDS ? (size_t)(3 * n + 3 * std::max(sc.nlights, 1)) * sizeof(float4) : 0;
     if (g.wpb == 16 && lds < 81 * 1024) lds = 81 * 1024;   // > half the CU's 160 KiB: one block per CU
     hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.gstride, first,
@@ -1503,6 +1505,8 @@ extern "C" int spt_scene_create(const rt_sphere *spheres, unsigned nspheres, spt
         if (!((q.e.x == 0.f) && (q.e.x == 0.f) && (q.e.z == 0.f))) lights.push_back(i);  // vec.h:44
     }
     sc->nlights = (int)lights.size();
+    if (lights.empty())                    // one zero record (render_kernel loads light 0 unconditionally)
+        soa.insert(soa.end(), 3, make_float4(0.f, 0.f, 0.f, 0.f));
     for (int i : lights) {                 // light records: geo, col, emi of each light, ascending
         const float4 g = soa[i], c = soa[2 * (size_t)n + i], e = soa[(size_t)n + i];
         soa.push_back(g);
@@ -1635,7 +1639,7 @@ int scene_render(const spt_scene *sc, const rt_camera *camera, float *d_colors, 
         launch_mode<rt::smallpt::GEO_BVH>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in,
                                           d_seeds_out, d_pixels, w, h, row_begin, row_end, first_sample,
                                           nsamples, cnt);
-    else if ((size_t)(3 * sc->n + 3 * sc->nlights) * sizeof(float4) <= (size_t)rt::smallpt::MAX_LDS_BYTES &&
+    else if ((size_t)(3 * sc->n + 3 * std::max(sc->nlights, 1)) * sizeof(float4) <= (size_t)rt::smallpt::MAX_LDS_BYTES &&
              !sc->force_global)
         launch_mode<rt::smallpt::GEO_LDS>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
                              d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);

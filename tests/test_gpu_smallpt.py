@@ -354,6 +354,32 @@ def test_random_scenes_vs_oracle(rt, oracle, seed):
     assert (g.seeds == f.seeds).all() and (g.pixels == f.pixels).all()
 
 
+@pytest.mark.parametrize("geo", ["lds", "global"])
+def test_light_free_scene_vs_oracle(rt, oracle, geo, monkeypatch):
+    """A scene with no emitter at all: render_kernel loads light 0's records
+    unconditionally (discarded by selects), so the scene carries one zero
+    record; the frame must still be the oracle's, bit for bit, on the LDS and
+    the global-SoA paths, both estimators."""
+    if geo == "global":
+        monkeypatch.setenv("RT_SPT_GEO", "global")
+    rng = np.random.default_rng(7)
+    n = 12
+    S = (rt.Sphere * n)()
+    for i in range(n):
+        rt.scenes._sphere(S[i], float(10 ** rng.uniform(-1, 1.2)), tuple(rng.uniform(-30, 30, 3)), (0.0, 0.0, 0.0),
+                          tuple(rng.uniform(0.1, 0.95, 3)), int(rng.choice([0, 1, 2])))
+    w, h = 40, 28
+    cam = rt.Camera()
+    cam.orig = rt.Vec3(0.0, 0.0, 80.0)
+    cam.target = rt.Vec3(0.0, 0.0, 0.0)
+    rt.scenes.update_camera(cam, w, h)
+    for mode in (0, 1):
+        f = rt.SmallptFrame(w, h, spheres=S, nspheres=n, camera=cam, mode=mode)
+        f.render(3)
+        _check((f.colors, f.seeds, f.pixels, f.counters),
+               _oracle_frame(oracle, w, h, [3], mode=mode, spheres=(S, n), cam=cam))
+
+
 def test_pack_pixels_matches_render(rt):
     """spt_pack_pixels_async (the repack after a multi-GPU colour all-gather)
     rebuilds exactly the pixels the render kernel wrote, for a row window."""
