@@ -708,7 +708,12 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         bool shadow = false;   // ray is the shadow ray of light li (DUAL: a shadow ray (hit, sdir) is pending)
         v3 sdir = mk(0.f, 0.f, 0.f);   // DUAL: the pending shadow ray's direction (origin: hit)
         bool fin = false;      // DUAL: the sample ends once its pending shadow ray is resolved
-        v3 hit, nl;            // the last hit point and its oriented normal (SampleLights' args)
+        // The last hit point IS the next ray's origin: every ray after a hit
+        // (bounce, mirror, refraction, shadow) starts there, and a camera
+        // ray's origin is written into it when the old hit is dead.  One
+        // register triple instead of copying hit into ray.o on four paths.
+        v3 &hit = ray.o;
+        v3 nl;                 // the last hit's oriented normal (SampleLights' args)
         v3 lsum;               // SampleLights' running result
         float lmax = 0.f;      // shadow ray maxt (len - EPSILON)
         float lw = 0.f;        // that light's weight s (geomfunc.h:159)
@@ -759,8 +764,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     const v3 u = vsmul(cs1 * r2s, vn);
                     v3 nd = vadd(u, vsmul(sn1 * r2s, v));
                     nd = vadd(nd, vsmul(sqrt_exact(1 - x2), wv));
-                    ray.o = hit;
-                    ray.d = nd;
+                    ray.d = nd;                          // origin: hit
                 } else {
                     v3 rorig = vsmul(0.1f, rdir);
                     rorig = vadd(rorig, mk(cam.orig.x, cam.orig.y, cam.orig.z));
@@ -864,8 +868,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 } else {
                     SPT_PROF(PB_NEAREST);
                     const float4 og = S.geo[id], oe = S.emi[id], oc = S.col[id];
-                    hit = vsmul(t, ray.d);
-                    hit = vadd(ray.o, hit);
+                    hit = vadd(ray.o, vsmul(t, ray.d)); // ray.o + ray.d * t (hit aliases ray.o)
                     v3 normal = vsub(hit, mk(og.x, og.y, og.z));
                     normal = vnorm(normal);
                     dp = vdot(normal, ray.d);
@@ -892,8 +895,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                         v3 nd = vsmul(2.f * vdot(normal, ray.d), normal);
                         nd = vsub(ray.d, nd);
                         thr = vmul(thr, mk(oc.x, oc.y, oc.z));
-                        ray.o = hit;
-                        ray.d = nd;
+                        ray.d = nd;                             // origin: hit
                     } else {
                         SPT_PROF(PB_REFR);
                         specular = true;
@@ -988,8 +990,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                             if (DUAL) {
                                 sdir = vn;                      // queried next iteration, with the bounce ray
                             } else {
-                                ray.o = hit;
-                                ray.d = vn;
+                                ray.d = vn;                     // origin: hit
                             }
                             lmax = len - EPS;
                             lw = quo;
@@ -1005,8 +1006,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                         const float4 oc = S.col[id];
                         v3 nd = vsmul(2.f * dp, normal);         // vdot(normal, ray.d) = dp
                         nd = vsub(ray.d, nd);
-                        ray.o = hit;
-                        if (tir) {
+                        if (tir) {                              // origin: hit
                             thr = vmul(thr, mk(oc.x, oc.y, oc.z));
                             ray.d = nd;
                         } else {
