@@ -605,6 +605,10 @@ __device__ __forceinline__ int to_int(float x)
 #endif
 constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2;
 
+#ifndef RT_SPT_DUAL_MINWAVES
+#define RT_SPT_DUAL_MINWAVES 7   // the uncounted two-query kernel: 85 -> 72 VGPRs (no VGPR spills; a few SGPRs spill
+                                 // to VGPR lanes), occupancy 5 -> 7: Cornell 1080p 17.87 -> 17.3 ms
+#endif
 #ifndef RT_BVH_MINWAVES_COUNT
 #define RT_BVH_MINWAVES_COUNT 4   // the counted hierarchy kernels (not timed): room for the counters, no spills
 #endif
@@ -616,7 +620,8 @@ constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2;
 // (rad += thr * Ld, geomfunc.h:229-230) before it shades the bounce's hit.
 // One iteration per path vertex instead of two for a lit DIFF vertex.
 template <bool DL, bool COUNT, int GEO, bool DUAL = false>
-__global__ void __launch_bounds__(1024, GEO == 2 ? (COUNT ? RT_BVH_MINWAVES_COUNT : RT_BVH_MINWAVES) : RT_SPT_MINWAVES)
+__global__ void __launch_bounds__(1024, GEO == 2 ? (COUNT ? RT_BVH_MINWAVES_COUNT : RT_BVH_MINWAVES)
+                                              : ((DUAL && !COUNT) ? RT_SPT_DUAL_MINWAVES : RT_SPT_MINWAVES))
 render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,
               uint32_t *seeds_out, uint32_t *__restrict__ pixels, int w, int h,
@@ -1234,14 +1239,14 @@ void launch_mode(bool dl, bool count, const Shape &grid, hipStream_t s, const sp
                  float *colors, const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h,
                  int r0, int r1, int first, int ns, unsigned long long *cnt)
 {
-    // The two-query iteration for path tracing in single-light scenes, for
-    // windows of at most four waves per SIMD (a multi-GPU row band: the 16-
-    // wave block shape), where per-wave ILP is what is short: N = 8 band
-    // 2.87 -> 2.78 ms.  At full occupancy its 94 VGPRs (occupancy 5 instead
-    // of 6) cost more than the saved iterations: full frame 19.0 -> 19.6 ms.
-    // RT_SPT_DUAL=0 / 1 forces it off / on (A/B).
+    // The two-query iteration for path tracing in single-light scenes, at
+    // every launch shape: one iteration per lit DIFF vertex instead of two.
+    // Once the one-query kernel's copies were gone (hit aliasing ray.o, path
+    // state reset at sample end) it fits 72 VGPRs at occupancy 7 and beats
+    // the one-query form both where per-wave ILP is short (N = 8 band) and on
+    // the full frame (17.98 -> 17.3 ms).  RT_SPT_DUAL=0 / 1 forces it off / on (A/B).
     const int dual_env = getenv("RT_SPT_DUAL") ? atoi(getenv("RT_SPT_DUAL")) : -1;
-    const bool dual_ok = dual_env < 0 ? grid.wpb == 16 : dual_env != 0;
+    const bool dual_ok = dual_env != 0;
     if (dl) {
         if (count) launch<true, true, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
         else launch<true, false, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);

@@ -405,7 +405,7 @@ def test_pack_pixels_matches_render(rt):
 def test_one_and_two_query_iterations(rt, oracle, dual, monkeypatch):
     """Both forms of the single-light loop -- one ray query per iteration, and
     the two-query iteration (shadow ray + bounce ray together, which the
-    library picks for multi-GPU row bands) -- forced either way, against the
+    library picks for every single-light scene) -- forced either way, against the
     oracle at a small size and the reference-core golden at 1920x1080x64."""
     import json
     import os
