@@ -25,6 +25,7 @@ void release_state(DeviceState *st)
     if (st->wf_done) (void)hipEventSynchronize(st->wf_done);
     for (int i = 0; i < NSCRATCH; i++)
         if (st->buf[i]) (void)hipFree(st->buf[i]);
+    if (st->pool_ovf) (void)hipHostFree(st->pool_ovf);   // host-mapped overflow flags
     if (st->wf_done) (void)hipEventDestroy(st->wf_done);
     if (st->stream) (void)hipStreamDestroy(st->stream);
     delete st;
@@ -129,6 +130,13 @@ double pool_fraction(DeviceState &st, int which, long long trees, double initial
     while (i < POOL_FITS && !(st.pool_fit[i].which == which && st.pool_fit[i].trees == trees)) i++;
     volatile int *flag;
     if (i == POOL_FITS) {                          // a new size: replace the oldest entry
+        // A frame of the evicted size may still be in flight and raise the
+        // slot's flag after it is cleared (a spurious growth of the new
+        // entry): wait for it first (eviction is rare).
+        if (st.wf_pending) {
+            (void)hipEventSynchronize(st.wf_done);
+            st.wf_pending = false;
+        }
         i = st.pool_fit_next;
         st.pool_fit_next = (i + 1) % POOL_FITS;
         st.pool_fit[i].which = which;
@@ -196,7 +204,7 @@ extern "C" int rt_set_device(int device)
 
 extern "C" int rt_release(void)
 {
-    rtrt::release_cached_scenes();
+    rtrt::release_cached_scenes();        // under each device state's lock
     std::lock_guard<std::mutex> lk(rtrt::g_mu);
     for (int d = 0; d < 64; d++) {
         if (rtrt::g_states[d]) {

@@ -256,6 +256,8 @@ struct BvhView {
     const float4 *ageo;   // "always" spheres (tested first)
     const int *aid;
     int nalways, nnodes;
+    const uint4 *wnode;   // the 8-wide layout (spt_bvh.h WideBuild: 7 x 16 B per node), staged in LDS
+    int wnodes, wdepth;   //   its node count and depth (levels of wide nodes)
 };
 constexpr float BVH_ALPHA_R = 1.f / 64.f;   // per node, with BETA, in the node record
 #ifndef RT_BVH_K
@@ -316,8 +318,13 @@ __device__ unsigned long long g_bvh_stats[24];
 struct BvhWalk {
     float t;
     int id, node, pend;
+    unsigned m;             // 8-wide walk: node = the current node (-1: root not yet visited), m = its
+    int sp;                 //   children still to visit (visit order), sp = stacked (node, mask) entries
 #if RT_BVH_PEND2
     int pend2;              // a second crossed leaf (only while pend holds one)
+#endif
+#ifdef RT_SPT_TRACE
+    unsigned tr_leaf, tr_trips, tr_leafruns;   // tools-only phase stamps (s_memtime cycles, counts)
 #endif
 };
 
@@ -440,6 +447,10 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
             64 * __builtin_popcountll(pm) < RT_BVH_BATCH * __builtin_popcountll(pm | sm))
             continue;
 #endif
+#ifdef RT_SPT_TRACE
+        const unsigned long long tr_l0 = __builtin_amdgcn_s_memtime();
+        W.tr_leafruns++;
+#endif
         if (pend != 0) {
             const int f = pend & 0xffffff, c = pend >> 24;
             BVH_ST(1, 1);
@@ -525,8 +536,14 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
             pend = 0;
 #endif
         }
+#ifdef RT_SPT_TRACE
+        W.tr_leaf += (unsigned)(__builtin_amdgcn_s_memtime() - tr_l0);
+#endif
         if (trips >= RT_BVH_BUDGET) break;
     }
+#ifdef RT_SPT_TRACE
+    W.tr_trips += trips;
+#endif
     W.t = t;
     W.id = id;
     W.node = node;
@@ -554,6 +571,220 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
     return node >= B.nnodes && pend == 0;
 }
 
+// ---------------------------------------------------------------------------
+// 8-wide hierarchy in LDS (GEO_WIDE; spt_bvh.h WideBuild).  The binary tree
+// above collapsed to 8 children per node with the child boxes quantised to 8
+// bits per plane (rounded outward on the host): configs[4]'s 10k spheres,
+// leaves of <= 8, make 528 nodes = 59 KB, which every block stages in LDS.
+// A query visits ~7 wide nodes instead of ~15 binary ones, and each visit is
+// an LDS read instead of a dependent L2 access: the binary walk's trip cost
+// ~1,300 cycles even with its wave alone on the chip (tools/c5_phase.py), its
+// latency, not contention, set configs[4]'s critical path.
+//
+// Culling is the binary walk's rule with the margin taken over the node: a
+// child box is skipped when the ray misses it grown by m = alpha * (|o - p| +
+// D0) + K, where |o - p| + D0 >= |o - C| for every child centre C and K is the
+// largest child's ALPHA_R * R + BETA -- m is at least each child's own binary
+// margin.  The slab test in the node's quantisation frame rounds within
+// ~2^-22 (|o - p| + D0) of the exact box planes, far inside alpha's factor-2
+// slack.  Visit order: the child in slot p ^ octant at position p (the host
+// put each octant's front child in the slot of that octant); the per-lane
+// stack holds (node << 8 | remaining mask) entries in LDS, one per level.
+__device__ __forceinline__ unsigned wide_visit(const uint4 *__restrict__ N, const ray3 &r, float ix, float iy,
+                                               float iz, float alpha, int oct, float lim)
+{
+    const uint4 h0 = N[0];
+    const float2 h1 = *(const float2 *)(N + 1);
+    const float cx = __uint_as_float(h0.x) - r.o.x, cy = __uint_as_float(h0.y) - r.o.y,
+                cz = __uint_as_float(h0.z) - r.o.z;
+    const float dist = __builtin_amdgcn_sqrtf(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, cz * cz)));
+    const float m = __builtin_fmaf(alpha, dist + h1.x, h1.y);
+    const float ax = __uint_as_float((h0.w & 255u) << 23) * ix;
+    const float ay = __uint_as_float(((h0.w >> 8) & 255u) << 23) * iy;
+    const float az = __uint_as_float(((h0.w >> 16) & 255u) << 23) * iz;
+    const float bx = cx * ix, by = cy * iy, bz = cz * iz;
+    const float mx = m * fabsf(ix), my = m * fabsf(iy), mz = m * fabsf(iz);
+    const float bnx = bx - mx, bfx = bx + mx, bny = by - my, bfy = by + my, bnz = bz - mz, bfz = bz + mz;
+    const unsigned valid = h0.w >> 24;
+    // The child boxes, a half (four slots) at a time: words 16 + 6 h ..
+    // 21 + 6 h hold lo_x, lo_y, lo_z, hi_x, hi_y, hi_z of slots 4h .. 4h+3.
+    // The near plane of an axis is the low byte for a positive direction.
+    const unsigned *W = (const unsigned *)N;
+    unsigned hm = 0;
+#pragma unroll
+    for (int hf = 0; hf < 2; hf++) {
+        const unsigned *q = W + 16 + 6 * hf;
+        const unsigned lx = q[0], ly = q[1], lz = q[2], ux = q[3], uy = q[4], uz = q[5];
+        const unsigned nxw = (oct & 1) ? ux : lx, fxw = (oct & 1) ? lx : ux;
+        const unsigned nyw = (oct & 2) ? uy : ly, fyw = (oct & 2) ? ly : uy;
+        const unsigned nzw = (oct & 4) ? uz : lz, fzw = (oct & 4) ? lz : uz;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int sh = 8 * j, sl = 4 * hf + j;
+            const float tnx = __builtin_fmaf((float)((nxw >> sh) & 255u), ax, bnx);
+            const float tfx = __builtin_fmaf((float)((fxw >> sh) & 255u), ax, bfx);
+            const float tny = __builtin_fmaf((float)((nyw >> sh) & 255u), ay, bny);
+            const float tfy = __builtin_fmaf((float)((fyw >> sh) & 255u), ay, bfy);
+            const float tnz = __builtin_fmaf((float)((nzw >> sh) & 255u), az, bnz);
+            const float tfz = __builtin_fmaf((float)((fzw >> sh) & 255u), az, bfz);
+            const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.f));
+            const float tf = fminf(fminf(tfx, tfy), fminf(tfz, lim));
+            hm |= ((tn <= tf && ((valid >> sl) & 1u)) ? 1u : 0u) << (sl ^ oct);
+        }
+    }
+    return hm;
+}
+
+#ifndef RT_WIDE_BUDGET
+#define RT_WIDE_BUDGET 16   // wide-walk trips per render-loop iteration before a lane's query is suspended
+#endif
+constexpr int WIDE_WORDS = 28;   // per node (spt_bvh.h)
+
+template <bool COUNT>
+__device__ __forceinline__ void wide_begin(const BvhView &B, const ray3 &r, bool shadow, float t, BvhWalk &W)
+{
+    bvh_begin<COUNT>(B, r, shadow, t, W);
+    W.node = -1;                                        // the root is visited by the first trip
+    W.m = (!COUNT && shadow && W.id >= 0) ? 0u : 1u;
+    W.sp = 0;
+}
+
+// Advances the wave's wide walks by up to RT_WIDE_BUDGET trips; returns true
+// for a lane whose query is complete (results as bvh_walk).  L: the block's
+// LDS copy of the nodes; stk: this wave's LDS stack (entry k of lane l at
+// stk[64 k + l]).  Crossed leaves are postponed and tested together as in
+// bvh_walk (two pending per lane); a leaf of more than four spheres is tested
+// four at a time.
+template <bool COUNT>
+__device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigned *__restrict__ stk, const ray3 &r,
+                          bool shadow, BvhWalk &W)
+{
+    const float maxt = W.t;
+    float t = W.t;
+    int id = W.id, cur = W.node, pend = W.pend, pend2 = W.pend2, sp = W.sp;
+    unsigned m = W.m;
+    const float dx = fabsf(r.d.x) < 1e-30f ? copysignf(1e-30f, r.d.x) : r.d.x;
+    const float dy = fabsf(r.d.y) < 1e-30f ? copysignf(1e-30f, r.d.y) : r.d.y;
+    const float dz = fabsf(r.d.z) < 1e-30f ? copysignf(1e-30f, r.d.z) : r.d.z;
+    const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
+    const float e = fabsf(r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z - 1.f);
+    const float alpha = e < 0x1p-16f ? BVH_K * (1.04e-3f + __builtin_amdgcn_sqrtf(e + 0x1p-22f)) : 1e30f;
+    const int oct = (dx < 0.f ? 1 : 0) | (dy < 0.f ? 2 : 0) | (dz < 0.f ? 4 : 0);
+    const unsigned *Lw = (const unsigned *)L;
+    unsigned *my = stk + (threadIdx.x & 63);
+    int trips = 0;
+    while (true) {
+        if (m != 0 && pend2 == 0) {
+            int cw;
+            if (cur < 0) {
+                cw = 0;                                  // the root
+                m = 0;
+            } else {
+                const int p = __builtin_ctz(m);
+                m &= m - 1;
+                cw = (int)Lw[cur * WIDE_WORDS + 8 + (p ^ oct)];
+            }
+            if (cw < 0) {
+                if (pend == 0) pend = ~cw;
+                else pend2 = ~cw;
+            } else {
+                const unsigned hm = wide_visit(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t);
+                if (hm) {
+                    if (m) {
+                        my[64 * sp] = ((unsigned)cur << 8) | m;
+                        sp++;
+                    }
+                    cur = cw;
+                    m = hm;
+                }
+            }
+            if (m == 0 && sp > 0) {
+                sp--;
+                const unsigned e2 = my[64 * sp];
+                cur = (int)(e2 >> 8);
+                m = e2 & 255u;
+            }
+        }
+        trips++;
+        const unsigned long long pm = __builtin_amdgcn_ballot_w64(pend != 0);
+        const unsigned long long sm = __builtin_amdgcn_ballot_w64(m != 0 && pend2 == 0);
+        if (pm == 0) {
+            if (sm == 0 || trips >= RT_WIDE_BUDGET) break;
+            continue;
+        }
+        if (sm != 0 && trips < RT_WIDE_BUDGET &&
+            64 * __builtin_popcountll(pm & ~sm) < RT_BVH_BATCH * __builtin_popcountll(pm | sm))
+            continue;
+        if (pend != 0) {
+            const int f = pend & 0xffffff, c = pend >> 24, c4 = c < BVH_LEAF_MAX ? c : BVH_LEAF_MAX;
+            float4 g[BVH_LEAF_MAX];
+#pragma unroll
+            for (int q = 0; q < BVH_LEAF_MAX; q++)        // all loads first: one latency per leaf
+                g[q] = B.geo[f + (q < c4 ? q : 0)];
+            float dq[BVH_LEAF_MAX];
+            bool bad = false;
+#pragma unroll
+            for (int q = 0; q < BVH_LEAF_MAX; q++) {
+                const float opx = g[q].x - r.o.x, opy = g[q].y - r.o.y, opz = g[q].z - r.o.z;
+                const float bb = opx * r.d.x + opy * r.d.y + opz * r.d.z;
+                const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g[q].w;
+                bad = bad || (q < c4 && fabsf(det) < 0x1p-96f);
+                const float sd = sqrt_nr(det);
+                const float t1 = bb - sd, t2 = bb + sd;
+                dq[q] = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
+            }
+            if (wave_any(bad)) {
+#pragma unroll
+                for (int q = 0; q < BVH_LEAF_MAX; q++) dq[q] = sphere_hit(g[q], r);
+            }
+            int bpos = -1;
+#pragma unroll
+            for (int q = 0; q < BVH_LEAF_MAX; q++) {
+                if (q < c4) {
+                    const float d = dq[q];
+                    if (shadow) {
+                        if (d < maxt) {
+                            if (COUNT) {
+                                const int i = B.id[f + q];
+                                if (i > id) id = i;
+                            } else {
+                                bpos = f + q;
+                            }
+                        }
+                    } else if (d < t) {
+                        t = d;
+                        bpos = f + q;
+                    } else if (d == t) {
+                        const int cur_id = bpos >= 0 ? B.id[bpos] : id;
+                        if (B.id[f + q] > cur_id) bpos = f + q;
+                    }
+                }
+            }
+            if (bpos >= 0) id = B.id[bpos];
+            if (c > BVH_LEAF_MAX) {
+                pend = (f + BVH_LEAF_MAX) | ((c - BVH_LEAF_MAX) << 24);
+            } else {
+                pend = pend2;
+                pend2 = 0;
+            }
+            if (!COUNT && shadow && id >= 0) {
+                m = 0;
+                sp = 0;
+                pend = pend2 = 0;
+            }
+        }
+        if (trips >= RT_WIDE_BUDGET) break;
+    }
+    W.t = t;
+    W.id = id;
+    W.node = cur;
+    W.m = m;
+    W.sp = sp;
+    W.pend = pend;
+    W.pend2 = pend2;
+    return m == 0 && pend == 0;
+}
+
 struct Counts { unsigned long long isect, isectp, tests, samples; };
 
 // Tools-only block profile (build with -DRT_SPT_PROF; tools/ab.py PROF=1):
@@ -574,10 +805,17 @@ __device__ unsigned long long g_spt_prof[2 * PB_N];
 
 // Tools-only wave timeline (build with -DRT_SPT_TRACE): per wave of the grid
 // {start, end} (s_memrealtime, 100 MHz), HW_ID, XCC_ID and {sum, max} over
-// its lanes of the loop iterations, at g_spt_trace[2 * (linear block * 4 +
+// its lanes of the loop iterations, at g_spt_trace[4 * (linear block * 4 +
 // wave) + 0/1].  Never in the product build.
+// Phase stamps (s_memtime, shader clock), hierarchy kernels: per wave, the
+// max over its lanes of the cycles spent in the walk (bvh_begin + bvh_walk),
+// of those in leaf blocks, walk trips, leaf-block passes and queries; at
+// g_spt_trace[4 * wave + 2/3].  g_spt_only_group >= 0 renders only that tile
+// group (the other waves exit at once): the group's waves run alone on the
+// chip, which splits contention from latency.
 #ifdef RT_SPT_TRACE
 __device__ uint4 *g_spt_trace;
+__device__ int g_spt_only_group = -1;
 #endif
 
 // toInt, vec.h:62 (clamp macro keeps -0.0; glibc powf via rt_glibc_math.h).
@@ -603,7 +841,17 @@ __device__ __forceinline__ int to_int(float x)
 #define RT_BVH_MINWAVES 6   // the hierarchy (GEO_BVH) kernels: 93 -> 80 VGPRs (2 spilled), occupancy 5 -> 6: the
                             // latency-bound walk gains more from the sixth wave than the spills cost (-10 %)
 #endif
-constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2;
+constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2, GEO_WIDE = 3;
+#ifndef RT_WIDE_PERSIST
+#define RT_WIDE_PERSIST 1   // 8-wide kernels: persistent waves taking tiles from a work counter (A/B: 0 = a wave per tile)
+#endif
+#ifndef RT_WIDE_MINWAVES
+#define RT_WIDE_MINWAVES 4  // the 8-wide (LDS) hierarchy kernels: 126 VGPRs unbounded; 5 or 6 waves per SIMD spill
+#endif
+#ifndef RT_SPT_GSTORE
+#define RT_SPT_GSTORE 1     // hierarchy kernels: a group's outputs stored whole by its last wave (A/B: 0)
+#endif
+constexpr int GS_BYTES = 6160;      // per tile group: 8 x 96 colour floats, 8 x 64 seed words, 8 x 32 pixels, count
 
 #ifndef RT_SPT_DUAL_MINWAVES
 #define RT_SPT_DUAL_MINWAVES 7   // the uncounted two-query kernel: 85 -> 72 VGPRs (no VGPR spills; a few SGPRs spill
@@ -621,6 +869,7 @@ constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2;
 // One iteration per path vertex instead of two for a lit DIFF vertex.
 template <bool DL, bool COUNT, int GEO, bool DUAL = false>
 __global__ void __launch_bounds__(1024, GEO == 2 ? (COUNT ? RT_BVH_MINWAVES_COUNT : RT_BVH_MINWAVES)
+                                              : GEO == 3 ? (COUNT ? RT_BVH_MINWAVES_COUNT : RT_WIDE_MINWAVES)
                                               : ((DUAL && !COUNT) ? RT_SPT_DUAL_MINWAVES : RT_SPT_MINWAVES))
 render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,
@@ -629,12 +878,14 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
               int prio_sched, const int *__restrict__ group_order, unsigned *__restrict__ group_cost,
               const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
               const float4 *__restrict__ g_col, const float4 *__restrict__ g_lrec, int nlights,
-              BvhView bvh, unsigned long long *__restrict__ counters)
+              BvhView bvh, unsigned long long *__restrict__ counters, int *__restrict__ work)
 {
     constexpr bool LDS = GEO == GEO_LDS;
-#ifdef RT_SPT_TRACE
-    const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();
-#endif
+    // GEO_WIDE: persistent waves -- each wave takes 8x8 tiles from a work
+    // counter (in the adaptive order's slot sequence, heaviest groups first)
+    // until the window is done, so a block's LDS copy of the hierarchy is
+    // made once and a CU never idles behind one block's slowest wave.
+    constexpr bool PERSIST = GEO == GEO_WIDE && RT_WIDE_PERSIST;
     // Dynamic LDS carve (16-B multiples): geo | emi | col (n each) | lrec (3 per light),
     // a copy of the scene's global SoA (spt_scene_create).
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -651,6 +902,16 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     S.nlights = nlights;
     S.n = nspheres;
     const DynGeo geo{S.geo, S.n};
+    // GEO_WIDE LDS carve: the wide nodes (7 x 16 B each), then per wave of the
+    // block its lanes' stacks ((wdepth - 1) entries x 64 lanes x 4 B).
+    const uint4 *wL = (const uint4 *)smem;
+    unsigned *wstk = nullptr;
+    if (GEO == GEO_WIDE) {
+        uint4 *d = (uint4 *)smem;
+        for (int i = threadIdx.x; i < 7 * bvh.wnodes; i += blockDim.x) d[i] = bvh.wnode[i];
+        wstk = (unsigned *)(smem + (size_t)112 * bvh.wnodes) + (size_t)(threadIdx.x >> 6) * 64 * (bvh.wdepth - 1);
+        __syncthreads();
+    }
 
     // 8x8 pixel tiles of the row window, one per wave, in groups of four
     // side by side (a 32x8 strip: whole 128-B lines of the seed, colour and
@@ -664,22 +925,48 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // Compiled into the hierarchy kernels only: in the full-scan kernels
     // (Cornell) the order/cost plumbing cost 1.4 % of the frame and 8 % of an
     // N = 8 band (measured A/B) although it is never used there.
-    constexpr bool SCHED = GEO == GEO_BVH;
-    const int slot = (wave >> 2) * (int)gridDim.x + (int)blockIdx.x;
-    const int grp = (SCHED && group_order) ? group_order[slot] : slot;
-    const int tile = grp * 4 + (wave & 3);
-    unsigned long long t_start = 0;
-    if (SCHED) t_start = __builtin_amdgcn_s_memrealtime();
-    const int x = (tile % tiles_x) * 8 + (lane & 7);
-    // gstride > 1: the window is every gstride-th 8-row group from row_begin
-    // (spt_scene_render_groups_async, multi-GPU load balance).
-    const int y = row_begin + (tile / tiles_x) * 8 * gstride + (lane >> 3);
-    const bool active = tile < ntiles && x < w && y < row_end;
-
+    constexpr bool SCHED = GEO == GEO_BVH || GEO == GEO_WIDE;
     Counts cnt = {0, 0, 0, 0};
 #ifdef RT_SPT_PROF
     unsigned prof_l[PB_N] = {}, prof_w[PB_N] = {};
 #endif
+    // Work item f: tile (f & 3) of dispatch slot f >> 2.  Static launches: one
+    // item per wave, slot (wave >> 2) * gridDim.x + blockIdx.x.
+    const int nwork = 4 * ((ntiles + 3) >> 2);
+    int f = ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) * 4 + (wave & 3);
+    if (PERSIST) {
+        int v = 0;
+        if (lane == 0) v = atomicAdd(work, 1);
+        f = __shfl(v, 0, 64);
+    }
+    while (!PERSIST || f < nwork) {
+    const int slot = f >> 2;
+    const int grp = (SCHED && group_order) ? group_order[slot] : slot;
+    const int tile = grp * 4 + (f & 3);
+    unsigned long long t_start = 0;
+    if (SCHED) t_start = __builtin_amdgcn_s_memrealtime();
+    // GSTORE (hierarchy kernels): per group of the block a 32x8 staging
+    // strip in LDS -- colours, seeds, pixels -- and an arrival count.
+    // (Addresses recomputed where used: held across the loop they spilled.)
+    constexpr bool GSTORE = GEO == GEO_BVH && RT_SPT_GSTORE;
+#define GS_BASE() (smem + (size_t)((threadIdx.x >> 6) >> 2) * GS_BYTES)
+    if (GSTORE) {
+        if ((threadIdx.x & 255) == 0) *(int *)(GS_BASE() + 6144) = 0;
+        __syncthreads();
+    }
+    const int x = (tile % tiles_x) * 8 + (lane & 7);
+    // gstride > 1: the window is every gstride-th 8-row group from row_begin
+    // (spt_scene_render_groups_async, multi-GPU load balance).
+    const int y = row_begin + (tile / tiles_x) * 8 * gstride + (lane >> 3);
+#ifdef RT_SPT_TRACE
+    const bool active = tile < ntiles && x < w && y < row_end && (g_spt_only_group < 0 || grp == g_spt_only_group);
+    unsigned tr_walk = 0, tr_leaf = 0, tr_trips = 0, tr_leafruns = 0, tr_queries = 0;
+    const unsigned long long tr_c0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();
+#else
+    const bool active = tile < ntiles && x < w && y < row_end;
+#endif
+
 #ifdef RT_SPT_TRACE
     unsigned tr_iters = 0;
 #endif
@@ -726,6 +1013,9 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         int k = 0;
         bool need_cam = nsamples > 0, need_bounce = false;
         BvhWalk walk;          // GEO_BVH: the current query's walk state
+#ifdef RT_SPT_TRACE
+        walk.tr_leaf = walk.tr_trips = walk.tr_leafruns = 0;
+#endif
         bool walking = false;  //   and whether it is suspended mid-walk
         constexpr float nc = 1.f, nt = 1.5f;
 #if RT_SPT_PRIO
@@ -838,8 +1128,29 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 // Resumable walk: a lane whose query needs more than this
                 // iteration's step budget sits out the rest of the iteration
                 // and continues its walk in the next one.
+#ifdef RT_SPT_TRACE
+                const unsigned long long tr_w0 = __builtin_amdgcn_s_memtime();
+                tr_queries += !walking;
+#endif
                 if (!walking) bvh_begin<COUNT>(bvh, ray, shadow, t, walk);
                 walking = !bvh_walk<COUNT>(bvh, ray, shadow, walk);
+#ifdef RT_SPT_TRACE
+                tr_walk += (unsigned)(__builtin_amdgcn_s_memtime() - tr_w0);
+#endif
+                if (walking) continue;
+                t = walk.t;
+                id = walk.id;
+                first = id;                 // any hit: the highest occluder (COUNT)
+            } else if constexpr (GEO == GEO_WIDE) {
+#ifdef RT_SPT_TRACE
+                const unsigned long long tr_w0 = __builtin_amdgcn_s_memtime();
+                tr_queries += !walking;
+#endif
+                if (!walking) wide_begin<COUNT>(bvh, ray, shadow, t, walk);
+                walking = !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk);
+#ifdef RT_SPT_TRACE
+                tr_walk += (unsigned)(__builtin_amdgcn_s_memtime() - tr_w0);
+#endif
                 if (walking) continue;
                 t = walk.t;
                 id = walk.id;
@@ -1071,22 +1382,83 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 specular = true;
             }
         }
-        if (nsamples > 0) {
-            colors[3 * (size_t)i] = col.x;
-            colors[3 * (size_t)i + 1] = col.y;
-            colors[3 * (size_t)i + 2] = col.z;
-            pixels[(size_t)y * w + x] =
-                (uint32_t)(to_int(col.x) | (to_int(col.y) << 8) | (to_int(col.z) << 16));
+        if (GSTORE) {                                   // staged: the group's last wave stores it
+            float *gs_col = (float *)GS_BASE();
+            uint32_t *gs_seed = (uint32_t *)(GS_BASE() + 3072), *gs_px = (uint32_t *)(GS_BASE() + 5120);
+            const int c = (wave & 3) * 8 + (lane & 7), r = lane >> 3;
+            if (nsamples > 0) {
+                gs_col[r * 96 + 3 * c] = col.x;
+                gs_col[r * 96 + 3 * c + 1] = col.y;
+                gs_col[r * 96 + 3 * c + 2] = col.z;
+                gs_px[r * 32 + c] = (uint32_t)(to_int(col.x) | (to_int(col.y) << 8) | (to_int(col.z) << 16));
+            }
+            gs_seed[r * 64 + 2 * c] = s0;
+            gs_seed[r * 64 + 2 * c + 1] = s1;
+        } else {
+            if (nsamples > 0) {
+                colors[3 * (size_t)i] = col.x;
+                colors[3 * (size_t)i + 1] = col.y;
+                colors[3 * (size_t)i + 2] = col.z;
+                pixels[(size_t)y * w + x] =
+                    (uint32_t)(to_int(col.x) | (to_int(col.y) << 8) | (to_int(col.z) << 16));
+            }
+            seeds_out[2 * (size_t)i] = s0;
+            seeds_out[2 * (size_t)i + 1] = s1;
         }
-        seeds_out[2 * (size_t)i] = s0;
-        seeds_out[2 * (size_t)i + 1] = s1;
+#ifdef RT_SPT_TRACE
+        if (GEO == GEO_BVH) {
+            tr_leaf = walk.tr_leaf;
+            tr_trips = walk.tr_trips;
+            tr_leafruns = walk.tr_leafruns;
+        }
+#endif
     }
-    if (SCHED && group_cost && lane == 0)   // this wave's duration (100 MHz ticks), summed per group
+    if (GSTORE) {
+        // The group's four waves finish at different times (configs[4]: per-
+        // wave work varies 6x); each leaves its 8x8 tile in LDS and the last
+        // one stores the whole 32x8 strip, so every 128-B line of the colour,
+        // seed and pixel rows is written once, whole.  (Stored per wave, the
+        // 96-B colour and 32-B pixel row segments of a tile share lines with
+        // the neighbouring tiles' and reach HBM as partial lines when the
+        // neighbours finish much later: 71 MB written per frame for 50 MB.)
+        const float *gs_col = (const float *)GS_BASE();
+        const uint32_t *gs_seed = (const uint32_t *)(GS_BASE() + 3072), *gs_px = (const uint32_t *)(GS_BASE() + 5120);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        int old = 0;
+        if (lane == 0) old = atomicAdd((int *)(GS_BASE() + 6144), 1);
+        old = __shfl(old, 0, 64);
+        if (old == 3) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            // entry (row r, group column c) -> its pixel, or invalid
+            const auto pix = [&](int r, int c, int &xx, int &yy) {
+                const int tl = grp * 4 + (c >> 3);
+                xx = (tl % tiles_x) * 8 + (c & 7);
+                yy = row_begin + (tl / tiles_x) * 8 * gstride + r;
+                return tl < ntiles && xx < w && yy < row_end;
+            };
+            int xx, yy;
+            if (nsamples > 0) {
+#pragma unroll 4
+                for (int k = 0; k < 12; k++) {
+                    const int j = k * 64 + lane, r = j / 96, c3 = j % 96, c = c3 / 3;
+                    if (pix(r, c, xx, yy)) colors[3 * ((size_t)(h - yy - 1) * w + xx) + (c3 - 3 * c)] = gs_col[j];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int j = k * 64 + lane, r = j >> 5, c = j & 31;
+                    if (pix(r, c, xx, yy)) pixels[(size_t)yy * w + xx] = gs_px[j];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int j = k * 64 + lane, r = j >> 6, c2 = j & 63, c = c2 >> 1;
+                if (pix(r, c, xx, yy)) seeds_out[2 * ((size_t)(h - yy - 1) * w + xx) + (c2 & 1)] = gs_seed[j];
+            }
+        }
+    }
+#undef GS_BASE
+    if (SCHED && group_cost && lane == 0)   // this tile's duration (100 MHz ticks), summed per group
         atomicAdd(&group_cost[grp], (unsigned)(__builtin_amdgcn_s_memrealtime() - t_start));
-    if (COUNT) {
-        const unsigned long long c[4] = {cnt.isect, cnt.isectp, cnt.tests, cnt.samples};
-        flush_counters<4>(counters, c);
-    }
 #ifdef RT_SPT_TRACE
     {
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
@@ -1094,14 +1466,33 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, off, 64));
         const unsigned sum = (unsigned)wave_sum_u64(tr_iters);
-        const size_t wv = (size_t)blockIdx.x * (blockDim.x >> 6) + wave;
+        const size_t wv = (size_t)f;                       // one record per work item (tile)
+        const unsigned tr_tot = (unsigned)(__builtin_amdgcn_s_memtime() - tr_c0);
+        unsigned ph[6] = {tr_walk, tr_leaf, tr_trips, tr_leafruns, tr_queries, tr_tot};
+#pragma unroll
+        for (int q = 0; q < 6; q++)
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) ph[q] = max(ph[q], (unsigned)__shfl_xor((int)ph[q], off, 64));
         if (lane == 0 && g_spt_trace) {
-            g_spt_trace[2 * wv] = make_uint4((unsigned)tr_t0, (unsigned)t1, __builtin_amdgcn_s_getreg(0xF804),
+            g_spt_trace[4 * wv] = make_uint4((unsigned)tr_t0, (unsigned)t1, __builtin_amdgcn_s_getreg(0xF804),
                                              __builtin_amdgcn_s_getreg(0xF814));
-            g_spt_trace[2 * wv + 1] = make_uint4(sum, mx, 0u, 0u);
+            g_spt_trace[4 * wv + 1] = make_uint4(sum, mx, (unsigned)grp, ph[5]);
+            g_spt_trace[4 * wv + 2] = make_uint4(ph[0], ph[1], ph[2], ph[3]);
+            g_spt_trace[4 * wv + 3] = make_uint4(ph[4], 0u, 0u, 0u);
         }
     }
 #endif
+    if (!PERSIST) break;
+    {
+        int v = 0;
+        if (lane == 0) v = atomicAdd(work, 1);
+        f = __shfl(v, 0, 64);
+    }
+    }   // work items
+    if (COUNT) {
+        const unsigned long long c[4] = {cnt.isect, cnt.isectp, cnt.tests, cnt.samples};
+        flush_counters<4>(counters, c);
+    }
 #ifdef RT_SPT_PROF
 #pragma unroll
     for (int b = 0; b < PB_N; b++) {
@@ -1138,6 +1529,7 @@ __global__ void __launch_bounds__(256) pack_kernel(const float *__restrict__ col
 #include <string>
 #include <vector>
 #include "rt_runtime.h"
+#include "spt_bvh.h"
 
 // A prepared scene (spt_scene_create): device AoS copy for the per-block LDS
 // staging, device SoA + light list for scenes above the LDS budget.
@@ -1156,6 +1548,11 @@ struct SptSched {
     unsigned *d_cost = nullptr, *h_cost = nullptr;   // h_*: pinned
     int *d_order = nullptr, *h_order = nullptr;
     hipEvent_t ev = nullptr;
+    // d_order is never rewritten or freed once a stream capture has used it
+    // (the graph holds its address): it is retired instead and freed with
+    // the scene, and a fresh buffer takes the next order.
+    bool order_captured = false;
+    std::vector<int *> retired;
 };
 
 struct spt_scene {
@@ -1165,12 +1562,36 @@ struct spt_scene {
     rt_sphere *d_spheres = nullptr;   // n x 44 B
     float4 *d_soa = nullptr;          // geo | emi | col (n each) | light records (3 per light)
     int nlights = 0;
-    void *d_bvh = nullptr;            // nodes | geo | id | always geo | always id (large scenes)
+    void *d_bvh = nullptr;            // nodes | geo | id | always geo | always id | wide nodes (large scenes)
     rt::smallpt::BvhView bvh = {};
     std::vector<rt_sphere> host;
     bool force_global = false;        // RT_SPT_GEO=global: scalar-load path at any size (A/B)
     mutable SptSched sched;           // adaptive group order (hierarchy scenes)
+    // Work counters of the persistent (8-wide hierarchy) launches: a ring,
+    // one zeroed counter per launch, so launches in flight on several
+    // streams do not share one.
+    static constexpr int NWORK = 64;
+    int *d_work = nullptr;
+    mutable int work_next = 0;
 };
+
+namespace {
+// 8-wide hierarchy launches: blocks of WIDE_WPB waves (each holds its own
+// LDS copy of the nodes and its waves' stacks), one per CU at the kernel's
+// occupancy of 4 waves per SIMD.  RT_WIDE_WPB / RT_WIDE_BLOCKS: A/B.
+constexpr int WIDE_WPB = 16;
+constexpr size_t WIDE_LDS_MAX = 144 * 1024;
+int wide_wpb()
+{
+    const char *e = getenv("RT_WIDE_WPB");
+    const int v = e ? atoi(e) : WIDE_WPB;
+    return v >= 1 && v <= 16 ? v : WIDE_WPB;
+}
+size_t wide_lds_bytes(int wnodes, int wdepth, int wpb)
+{
+    return (size_t)112 * wnodes + (size_t)wpb * 256 * (wdepth > 1 ? wdepth - 1 : 1);
+}
+}  // namespace
 
 namespace {
 
@@ -1181,6 +1602,7 @@ namespace {
 // SIMD gets four waves, instead of the dispatcher's uneven 3..5 per SIMD.
 struct Shape {
     int tiles_x, ntiles, gstride, wpb, nblocks;
+    int nslots = 0;                   // dispatch slots (tile groups of four) the order / cost arrays cover
     const int *order = nullptr;       // adaptive schedule (render_kernel's group_order / group_cost)
     unsigned *cost = nullptr;
     int heavy16 = 0;                  // with order: heaviest slots kept at top priority, in 16s
@@ -1203,6 +1625,20 @@ Shape launch_shape(const spt_scene &sc, int w, int r0, int r1, int gstride = 1)
     g.wpb = (wps <= 4.0 || (wps > 6.0 && wps <= 8.0)) ? 16 : 4;
     if (const char *e = getenv("RT_SPT_WPB")) g.wpb = atoi(e) == 16 ? 16 : 4;   // A/B
     g.nblocks = (g.ntiles + g.wpb - 1) / g.wpb;
+    g.nslots = g.nblocks * (g.wpb / 4);
+    if (sc.bvh.wnode) {               // persistent waves: one block per CU (fewer for a small window)
+        g.wpb = wide_wpb();
+        g.nblocks = (g.ntiles + g.wpb - 1) / g.wpb;
+        g.nslots = (g.ntiles + 3) / 4;
+#if RT_WIDE_PERSIST
+        g.nblocks = std::min(sc.cus, g.nblocks);
+        if (const char *e = getenv("RT_WIDE_BLOCKS")) g.nblocks = std::max(1, atoi(e));   // A/B
+#else
+        g.wpb &= ~3;                  // static: whole groups per block, a slot per group
+        g.nblocks = (g.ntiles + g.wpb - 1) / g.wpb;
+        g.nslots = g.nblocks * (g.wpb / 4);
+#endif
+    }
     return g;
 }
 
@@ -1228,10 +1664,17 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     const int n = sc.n;
     const float4 *gg = sc.d_soa, *ge = gg + n, *gc = ge + n, *gl = gc + n;
     size_t lds = LDS ? (size_t)(3 * n + 3 * std::max(sc.nlights, 1)) * sizeof(float4) : 0;
+    if (GEO == rt::smallpt::GEO_BVH && RT_SPT_GSTORE) lds = (size_t)(g.wpb / 4) * rt::smallpt::GS_BYTES;
     if (g.wpb == 16 && lds < 81 * 1024) lds = 81 * 1024;   // > half the CU's 160 KiB: one block per CU
+    int *work = nullptr;
+    if (GEO == rt::smallpt::GEO_WIDE) {
+        lds = wide_lds_bytes(sc.bvh.wnodes, sc.bvh.wdepth, g.wpb);
+        work = sc.d_work + (sc.work_next++ % spt_scene::NWORK);
+        if (hipMemsetAsync(work, 0, sizeof(int), s) != hipSuccess) return;   // (check_launch reports it)
+    }
     hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.gstride, first,
-                       ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt);
+                       ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt, work);
 }
 
 template <int GEO>
@@ -1250,7 +1693,7 @@ void launch_mode(bool dl, bool count, const Shape &grid, hipStream_t s, const sp
     if (dl) {
         if (count) launch<true, true, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
         else launch<true, false, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
-    } else if (GEO != rt::smallpt::GEO_BVH && sc.nlights == 1 && dual_ok) {
+    } else if (GEO != rt::smallpt::GEO_BVH && GEO != rt::smallpt::GEO_WIDE && sc.nlights == 1 && dual_ok) {
         if (count) launch<false, true, GEO, true>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
         else launch<false, false, GEO, true>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
     } else {
@@ -1259,184 +1702,37 @@ void launch_mode(bool dl, bool count, const Shape &grid, hipStream_t s, const sp
     }
 }
 
-// ---- hierarchy build (host) for scenes of >= BVH_MIN spheres
-constexpr int BVH_MIN = 256, BVH_LEAF = rt::smallpt::BVH_LEAF_MAX, BVH_MAX_ALWAYS = 16;
-
-struct HostNode {
-    float lo[3], hi[3];
-    int left = -1, right = -1;   // children (inner) ...
-    int first = 0, count = 0;    // ... or the leaf's sphere range
-    int axis = 0;                // split axis (inner)
-    float margin = 0.f;
-};
-
-// Binned-SAH binary tree over sphere boxes (host, once per scene).
-struct BvhBuild {
-    const rt_sphere *sp;
-    std::vector<int> idx;
-    std::vector<HostNode> nodes;
-
-    void box(int i, float *lo, float *hi) const
-    {
-        const rt_sphere &q = sp[i];
-        const float c[3] = {q.p.x, q.p.y, q.p.z};
-        for (int k = 0; k < 3; k++) { lo[k] = c[k] - q.rad; hi[k] = c[k] + q.rad; }
-    }
-    float centre(int i, int k) const { return k == 0 ? sp[i].p.x : (k == 1 ? sp[i].p.y : sp[i].p.z); }
-    static float area(const float *lo, const float *hi)
-    {
-        const float x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
-        return x * y + y * z + z * x;
-    }
-
-    int build(int lo, int hi)
-    {
-        const int me = (int)nodes.size();
-        nodes.emplace_back();
-        HostNode nd;
-        float clo[3] = {1e30f, 1e30f, 1e30f}, chi[3] = {-1e30f, -1e30f, -1e30f};
-        for (int k = 0; k < 3; k++) { nd.lo[k] = 1e30f; nd.hi[k] = -1e30f; }
-        for (int j = lo; j < hi; j++) {
-            float a[3], b[3];
-            box(idx[j], a, b);
-            for (int k = 0; k < 3; k++) {
-                nd.lo[k] = std::min(nd.lo[k], a[k]);
-                nd.hi[k] = std::max(nd.hi[k], b[k]);
-                clo[k] = std::min(clo[k], centre(idx[j], k));
-                chi[k] = std::max(chi[k], centre(idx[j], k));
-            }
-        }
-        // Margin term ALPHA * R + BETA (R = half diagonal); BETA also covers
-        // the float rounding of the box corners and tiny absolute scales.
-        double d2 = 0, mag = 0;
-        for (int k = 0; k < 3; k++) {
-            d2 += (double)(nd.hi[k] - nd.lo[k]) * (nd.hi[k] - nd.lo[k]);
-            mag = std::max(mag, (double)std::max(fabsf(nd.lo[k]), fabsf(nd.hi[k])));
-        }
-        nd.margin = (float)(rt::smallpt::BVH_ALPHA_R * 0.5 * sqrt(d2) + 1e-3 + 1e-5 * mag);
-        const int n = hi - lo;
-        if (n <= BVH_LEAF) {
-            nd.first = lo;
-            nd.count = n;
-            nodes[me] = nd;
-            return me;
-        }
-        // SAH over 16 centroid bins per axis.
-        constexpr int NB = 16;
-        int best_ax = -1, best_b = 0;
-        float best_cost = 1e30f;
-        for (int ax = 0; ax < 3; ax++) {
-            const float ext = chi[ax] - clo[ax];
-            if (!(ext > 0.f)) continue;
-            int cnt[NB] = {};
-            float blo[NB][3], bhi[NB][3];
-            for (int q = 0; q < NB; q++)
-                for (int k = 0; k < 3; k++) { blo[q][k] = 1e30f; bhi[q][k] = -1e30f; }
-            for (int j = lo; j < hi; j++) {
-                int q = (int)((centre(idx[j], ax) - clo[ax]) / ext * NB);
-                q = std::min(std::max(q, 0), NB - 1);
-                float a[3], b[3];
-                box(idx[j], a, b);
-                cnt[q]++;
-                for (int k = 0; k < 3; k++) { blo[q][k] = std::min(blo[q][k], a[k]); bhi[q][k] = std::max(bhi[q][k], b[k]); }
-            }
-            float rlo[NB][3], rhi[NB][3];
-            int rc[NB];
-            float alo[3] = {1e30f, 1e30f, 1e30f}, ahi[3] = {-1e30f, -1e30f, -1e30f};
-            int ac = 0;
-            for (int q = NB - 1; q >= 1; q--) {
-                for (int k = 0; k < 3; k++) { alo[k] = std::min(alo[k], blo[q][k]); ahi[k] = std::max(ahi[k], bhi[q][k]); }
-                ac += cnt[q];
-                for (int k = 0; k < 3; k++) { rlo[q][k] = alo[k]; rhi[q][k] = ahi[k]; }
-                rc[q] = ac;
-            }
-            float llo[3] = {1e30f, 1e30f, 1e30f}, lhi[3] = {-1e30f, -1e30f, -1e30f};
-            int lc = 0;
-            for (int q = 0; q < NB - 1; q++) {
-                for (int k = 0; k < 3; k++) { llo[k] = std::min(llo[k], blo[q][k]); lhi[k] = std::max(lhi[k], bhi[q][k]); }
-                lc += cnt[q];
-                if (lc == 0 || rc[q + 1] == 0) continue;
-                const float cost = area(llo, lhi) * lc + area(rlo[q + 1], rhi[q + 1]) * rc[q + 1];
-                if (cost < best_cost) { best_cost = cost; best_ax = ax; best_b = q + 1; }
-            }
-        }
-        int mid;
-        if (best_ax >= 0) {
-            const int ax = best_ax;
-            const float ext = chi[ax] - clo[ax];
-            auto it = std::partition(idx.begin() + lo, idx.begin() + hi, [&](int i) {
-                int q = (int)((centre(i, ax) - clo[ax]) / ext * NB);
-                q = std::min(std::max(q, 0), NB - 1);
-                return q < best_b;
-            });
-            mid = (int)(it - idx.begin());
-            nd.axis = ax;
-        } else {
-            mid = lo + n / 2;   // all centres equal: any split
-        }
-        if (mid == lo || mid == hi) mid = lo + n / 2;
-        nd.left = build(lo, mid);
-        nd.right = build(mid, hi);
-        nodes[me] = nd;
-        return me;
-    }
-
-    // Depth-first layout for ray-direction octant `oct` (bit k set: d_k < 0):
-    // at each inner node the child on the near side of its split axis comes
-    // first; link = escape index (inner) or ~(first | count << 24) (leaf).
-    void emit(int node, int oct, std::vector<float4> &out) const
-    {
-        const HostNode &h = nodes[node];
-        const size_t me = out.size() / 2;
-        out.push_back(make_float4(0.5f * (h.lo[0] + h.hi[0]), 0.5f * (h.lo[1] + h.hi[1]), 0.5f * (h.lo[2] + h.hi[2]),
-                                  0.f));
-        out.push_back(make_float4(0.5f * (h.hi[0] - h.lo[0]), 0.5f * (h.hi[1] - h.lo[1]), 0.5f * (h.hi[2] - h.lo[2]),
-                                  h.margin));
-        int link;
-        if (h.left < 0) {
-            link = ~(h.first | (h.count << 24));
-        } else {
-            const HostNode &L = nodes[h.left], &R = nodes[h.right];
-            const bool l_low = L.lo[h.axis] + L.hi[h.axis] <= R.lo[h.axis] + R.hi[h.axis];
-            const bool neg = (oct >> h.axis) & 1;
-            const int c0 = (l_low != neg) ? h.left : h.right;
-            emit(c0, oct, out);
-            emit(c0 == h.left ? h.right : h.left, oct, out);
-            link = (int)(out.size() / 2);                   // escape: the node after this subtree
-        }
-        float f;
-        memcpy(&f, &link, 4);
-        out[2 * me].w = f;
-    }
-};
-
-// Builds the hierarchy into sc->d_bvh / sc->bvh (nothing for small scenes).
+// ---- hierarchy build (host, spt_bvh.h) for scenes of >= sptbvh::MIN_SPHERES spheres
+// Builds the hierarchy into sc->d_bvh / sc->bvh (nothing for small scenes):
+// the binary tree's eight octant layouts and, when a block's LDS can hold it
+// (two blocks of WIDE_WPB waves per CU), the 8-wide layout -- with the
+// smallest leaf size in {8, 12, 16} whose tree fits.
 int build_scene_bvh(spt_scene *sc, const rt_sphere *spheres)
 {
     const int n = sc->n;
-    if (n < BVH_MIN || getenv("RT_SPT_NO_BVH")) return RT_OK;
-    std::vector<float> rads(n);
-    for (int i = 0; i < n; i++) rads[i] = spheres[i].rad;
-    std::nth_element(rads.begin(), rads.begin() + n / 2, rads.end());
-    const float med = rads[n / 2];
-    std::vector<int> always, rest;
-    for (int i = 0; i < n; i++) {
-        if (spheres[i].rad > 64.f * med && (int)always.size() < BVH_MAX_ALWAYS) always.push_back(i);
-        else rest.push_back(i);
-    }
-    BvhBuild b;
-    b.sp = spheres;
-    b.idx = rest;
-    if (!rest.empty()) b.build(0, (int)rest.size());
-    const int nn = (int)b.nodes.size(), nb = (int)rest.size(), na = (int)always.size();
+    if (n < sptbvh::MIN_SPHERES || getenv("RT_SPT_NO_BVH")) return RT_OK;
+    std::vector<int> always;
+    sptbvh::BvhBuild b;
+    sptbvh::partition_and_build(spheres, n, always, b);
+    const int nn = (int)b.nodes.size(), nb = (int)b.idx.size(), na = (int)always.size();
     // Eight layouts (one per direction octant), each with layout-local links.
-    std::vector<float4> nodes;
+    std::vector<sptbvh::f4> nodes;
     nodes.reserve(2 * (size_t)nn * 8);
     for (int oct = 0; oct < 8; oct++) {
-        std::vector<float4> lay;
+        std::vector<sptbvh::f4> lay;
         lay.reserve(2 * (size_t)nn);
         if (nn) b.emit(0, oct, lay);
         nodes.insert(nodes.end(), lay.begin(), lay.end());
+    }
+    sptbvh::WideBuild wb;
+    bool wide = false;
+    const char *we = getenv("RT_SPT_WIDE");             // 0: the binary walk only (A/B, tests)
+    if (nn && !(we && atoi(we) == 0)) {
+        for (int lm : {8, 12, 16}) {
+            wb.leaf_max = lm;
+            wb.build(b);
+            if (wide_lds_bytes(wb.nnodes, wb.depth, wide_wpb()) <= WIDE_LDS_MAX) { wide = true; break; }
+        }
     }
     std::vector<float4> geo(nb + na);
     std::vector<int> ids(nb + na);
@@ -1447,12 +1743,15 @@ int build_scene_bvh(spt_scene *sc, const rt_sphere *spheres)
         ids[j] = i;
     }
     const size_t nb_bytes = sizeof(float4) * nodes.size(), g_bytes = sizeof(float4) * geo.size(),
-                 i_bytes = sizeof(int) * ids.size();
-    hipError_t e = hipMalloc(&sc->d_bvh, nb_bytes + g_bytes + i_bytes + 16);
+                 i_bytes = sizeof(int) * ids.size(), w_bytes = wide ? 4 * wb.words.size() : 0;
+    const size_t w_off = (nb_bytes + g_bytes + i_bytes + 15) & ~(size_t)15;
+    hipError_t e = hipMalloc(&sc->d_bvh, w_off + w_bytes + 16);
     char *base = (char *)sc->d_bvh;
     if (e == hipSuccess) e = hipMemcpy(base, nodes.data(), nb_bytes, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(base + nb_bytes, geo.data(), g_bytes, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(base + nb_bytes + g_bytes, ids.data(), i_bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && wide) e = hipMemcpy(base + w_off, wb.words.data(), w_bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && wide) e = hipMalloc(&sc->d_work, sizeof(int) * spt_scene::NWORK);
     if (e != hipSuccess) return rtrt::fail_hip(e, "spt_scene_create hierarchy upload");
     rt::smallpt::BvhView &v = sc->bvh;
     v.node = (const float4 *)base;
@@ -1462,6 +1761,9 @@ int build_scene_bvh(spt_scene *sc, const rt_sphere *spheres)
     v.aid = v.id + nb;
     v.nalways = na;
     v.nnodes = nn;
+    v.wnode = wide ? (const uint4 *)(base + w_off) : nullptr;
+    v.wnodes = wide ? wb.nnodes : 0;
+    v.wdepth = wide ? wb.depth : 0;
     return RT_OK;
 }
 
@@ -1544,9 +1846,11 @@ extern "C" int spt_scene_destroy(spt_scene *sc)
     if (sc->d_spheres) (void)hipFree(sc->d_spheres);
     if (sc->d_soa) (void)hipFree(sc->d_soa);
     if (sc->d_bvh) (void)hipFree(sc->d_bvh);
+    if (sc->d_work) (void)hipFree(sc->d_work);
     SptSched &q = sc->sched;
     if (q.d_cost) (void)hipFree(q.d_cost);
     if (q.d_order) (void)hipFree(q.d_order);
+    for (int *p : q.retired) (void)hipFree(p);
     if (q.h_cost) (void)hipHostFree(q.h_cost);
     if (q.h_order) (void)hipHostFree(q.h_order);
     if (q.ev) (void)hipEventDestroy(q.ev);
@@ -1563,7 +1867,7 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
     const char *e = getenv("RT_SPT_SCHED");
     if (!sc.bvh.node || (e && atoi(e) == 0)) return false;   // the full-scan kernels have no order/cost code
     SptSched &q = sc.sched;
-    const int nslots = g.nblocks * (g.wpb / 4);
+    const int nslots = g.nslots;
     if (!(q.w == w && q.h == h && q.r0 == r0 && q.r1 == r1 && q.gstride == gstride && q.ns == ns &&
           q.mode == mode && q.nslots == nslots && memcmp(&q.cam, &cam, sizeof(cam)) == 0)) {
         q.w = w; q.h = h; q.r0 = r0; q.r1 = r1; q.gstride = gstride; q.ns = ns; q.mode = mode;
@@ -1572,14 +1876,19 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
     }
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
-        if (q.state == 2) g.order = q.d_order;         // a device pointer: capture-safe
+        if (q.state == 2) {                            // a device pointer, kept alive and unchanged from now on
+            g.order = q.d_order;
+            q.order_captured = true;
+        }
         return false;
     }
     if (nslots > q.cap) {                               // grow (the old buffers may still be read)
         if (q.ev && hipEventSynchronize(q.ev) != hipSuccess) return false;
         if (hipStreamSynchronize(s) != hipSuccess) return false;
         if (q.d_cost) (void)hipFree(q.d_cost);
-        if (q.d_order) (void)hipFree(q.d_order);
+        if (q.d_order && q.order_captured) q.retired.push_back(q.d_order);
+        else if (q.d_order) (void)hipFree(q.d_order);
+        q.order_captured = false;
         if (q.h_cost) (void)hipHostFree(q.h_cost);
         if (q.h_order) (void)hipHostFree(q.h_order);
         q.d_cost = q.h_cost = nullptr;
@@ -1601,6 +1910,13 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
         for (int i = 0; i < nslots; i++) idx[i] = i;
         std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return q.h_cost[a] > q.h_cost[b]; });
         memcpy(q.h_order, idx.data(), sizeof(int) * nslots);
+        if (q.order_captured) {                        // a graph reads the old order: keep it, take a new buffer
+            int *fresh = nullptr;
+            if (hipMalloc(&fresh, sizeof(int) * q.cap) != hipSuccess) return false;
+            q.retired.push_back(q.d_order);
+            q.d_order = fresh;
+            q.order_captured = false;
+        }
         if (hipMemcpyAsync(q.d_order, q.h_order, sizeof(int) * nslots, hipMemcpyHostToDevice, s) != hipSuccess)
             return false;
         q.state = 2;
@@ -1640,7 +1956,11 @@ int scene_render(const spt_scene *sc, const rt_camera *camera, float *d_colors, 
     const bool record = sched_before(*sc, grid, s, w, h, row_begin, row_end, gstride, nsamples, mode, *camera);
     unsigned long long *cnt = (unsigned long long *)d_counters;
     const bool dl = mode == SPT_DIRECT_LIGHTING;
-    if (sc->bvh.node)
+    if (sc->bvh.wnode)
+        launch_mode<rt::smallpt::GEO_WIDE>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in,
+                                           d_seeds_out, d_pixels, w, h, row_begin, row_end, first_sample,
+                                           nsamples, cnt);
+    else if (sc->bvh.node)
         launch_mode<rt::smallpt::GEO_BVH>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in,
                                           d_seeds_out, d_pixels, w, h, row_begin, row_end, first_sample,
                                           nsamples, cnt);
@@ -1693,15 +2013,15 @@ namespace {
 // synchronises the device to free it on every call.
 struct SceneCache {
     std::vector<rt_sphere> host;
-    std::string hooks;                // the preparation's test hooks (RT_SPT_NO_BVH, RT_SPT_GEO)
+    std::string hooks;                // the preparation's test hooks (RT_SPT_NO_BVH, RT_SPT_GEO, RT_SPT_WIDE)
     spt_scene *sc = nullptr;
 };
 SceneCache g_scene_cache[64];
 
 std::string prep_hooks()
 {
-    const char *a = getenv("RT_SPT_NO_BVH"), *b = getenv("RT_SPT_GEO");
-    return std::string(a ? "1" : "0") + "|" + (b ? b : "");
+    const char *a = getenv("RT_SPT_NO_BVH"), *b = getenv("RT_SPT_GEO"), *c = getenv("RT_SPT_WIDE");
+    return std::string(a ? "1" : "0") + "|" + (b ? b : "") + "|" + (c ? c : "");
 }
 
 // Caller holds the device state's lock.
@@ -1732,9 +2052,23 @@ int cached_scene(const rtrt::DeviceState &st, const rt_sphere *spheres, unsigned
 }  // namespace
 
 namespace rtrt {
+// Under each device state's lock, the one cached_scene's callers hold: a
+// render on another thread never sees a destroyed cached scene.
 void release_cached_scenes()
 {
-    for (SceneCache &c : g_scene_cache) {
+    for (int d = 0; d < 64; d++) {
+        SceneCache &c = g_scene_cache[d];
+        DeviceState *st = nullptr;
+        if (c.sc) {
+            DeviceScope scope;
+            if (scope.select(d) == RT_OK && state(&st) == RT_OK) {
+                std::lock_guard<std::recursive_mutex> lk(st->mu);
+                if (c.sc) spt_scene_destroy(c.sc);
+                c.sc = nullptr;
+                c.host.clear();
+                continue;
+            }
+        }
         if (c.sc) spt_scene_destroy(c.sc);
         c.sc = nullptr;
         c.host.clear();
@@ -1811,6 +2145,13 @@ extern "C" int spt_trace_set(void *buf)
     uint4 *p = (uint4 *)buf;
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(rt::smallpt::g_spt_trace), &p, sizeof(p));
     return e == hipSuccess ? RT_OK : rtrt::fail_hip(e, "spt_trace_set");
+}
+
+// Tools-only: renders only tile group g (-1: all) in later launches.
+extern "C" int spt_trace_only_group(int g)
+{
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(rt::smallpt::g_spt_only_group), &g, sizeof(g));
+    return e == hipSuccess ? RT_OK : rtrt::fail_hip(e, "spt_trace_only_group");
 }
 #endif
 

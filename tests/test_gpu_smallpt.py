@@ -131,8 +131,15 @@ def test_large_scene_global_path(rt, oracle, env, monkeypatch):
     _check((f.colors, f.seeds, f.pixels, f.counters), ref)
 
 
+# The two hierarchy walks: the 8-wide LDS-resident tree (default for scenes
+# whose tree fits a block's LDS) and the binary octant-layout tree in global
+# memory (RT_SPT_WIDE=0; the path for larger trees).
+WALKS = [pytest.param({}, id="wide"), pytest.param({"RT_SPT_WIDE": "0"}, id="binary")]
+
+
+@pytest.mark.parametrize("walk", WALKS)
 @pytest.mark.parametrize("counted", [True, False])
-def test_configs4_full_size_golden(rt, oracle, counted):
+def test_configs4_full_size_golden(rt, oracle, counted, walk, monkeypatch):
     """BASELINE configs[4] at full size -- the 10k-sphere scene_build_complex
     scene, 1920x1080, 64 spp from the initial state -- through the hierarchy
     kernel (with and without the work counters), against the golden hashes of
@@ -140,6 +147,8 @@ def test_configs4_full_size_golden(rt, oracle, counted):
     oracle/_ref: geomfunc.h:71-110 Intersect / IntersectP)."""
     import json
     import os
+    for k, v in walk.items():
+        monkeypatch.setenv(k, v)
     gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
     g = gold["smallpt"]["1920x1080_64spp_complex10k"]
     spheres, n, cam = rt.scenes.complex10k()
@@ -220,8 +229,9 @@ def test_scene_cache_follows_the_array(rt, oracle):
         assert (f.colors.view(np.uint32) == ref_col.view(np.uint32)).all() and (f.pixels == ref_px).all()
 
 
+@pytest.mark.parametrize("walk", WALKS)
 @pytest.mark.parametrize("sched", ["0", "1"])
-def test_adaptive_group_order_is_exact(rt, monkeypatch, sched):
+def test_adaptive_group_order_is_exact(rt, monkeypatch, sched, walk):
     """Hierarchy scenes dispatch their tile groups heaviest-first once a
     launch has recorded the groups' wave times (SptSched): the 1st launch of a
     key records, the 2nd builds the order, the 3rd and later use it.  Every
@@ -230,6 +240,8 @@ def test_adaptive_group_order_is_exact(rt, monkeypatch, sched):
     import ctypes as C
     import torch
     monkeypatch.setenv("RT_SPT_SCHED", sched)
+    for k, v in walk.items():
+        monkeypatch.setenv(k, v)
     w, h = 480, 270
     spheres, n, cam = rt.scenes.complex10k()
     rt.scenes.update_camera(cam, w, h)
@@ -261,16 +273,18 @@ def test_adaptive_group_order_is_exact(rt, monkeypatch, sched):
 
 
 def _bvh_vs_scan(rt, monkeypatch, spheres, n, cam, w, h, spp, mode=0):
-    """Renders with the hierarchy and with the full scan (RT_SPT_NO_BVH),
-    each with and without the work counters (the uncounted kernels stop a
-    shadow query at its first occluder): colours, seeds, pixels and counters
-    must be identical bit for bit."""
+    """Renders with the 8-wide hierarchy, the binary hierarchy (RT_SPT_WIDE=0)
+    and the full scan (RT_SPT_NO_BVH), each with and without the work
+    counters (the uncounted kernels stop a shadow query at its first
+    occluder): colours, seeds, pixels and counters must be identical bit for
+    bit."""
     outs = []
-    for no_bvh in (False, True):
-        if no_bvh:
-            monkeypatch.setenv("RT_SPT_NO_BVH", "1")
-        else:
-            monkeypatch.delenv("RT_SPT_NO_BVH", raising=False)
+    for env in ({}, {"RT_SPT_WIDE": "0"}, {"RT_SPT_NO_BVH": "1"}):
+        for k in ("RT_SPT_WIDE", "RT_SPT_NO_BVH"):
+            if k in env:
+                monkeypatch.setenv(k, env[k])
+            else:
+                monkeypatch.delenv(k, raising=False)
         for counted in (True, False):
             f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n, camera=cam, mode=mode)
             f.render(spp, counters=counted)
@@ -279,7 +293,7 @@ def _bvh_vs_scan(rt, monkeypatch, spheres, n, cam, w, h, spp, mode=0):
     for b in outs[1:]:
         assert np.array_equal(a.colors.view(np.uint32), b.colors.view(np.uint32))
         assert np.array_equal(a.seeds, b.seeds) and np.array_equal(a.pixels, b.pixels)
-    assert a.counters == outs[2].counters
+    assert a.counters == outs[2].counters == outs[4].counters
 
 
 def test_bvh_equals_full_scan_configs4(rt, monkeypatch):

@@ -25,14 +25,14 @@ def run(L, sc, cam, seeds0, seeds, col, px, r0, r1, st):
     ntiles = ((W + 7) // 8) * ((r1 - r0 + 7) // 8)
     gx, gy = (ntiles + 15) // 16, 16           # blocks (upper bound), waves per block
     nw = gx * gy
-    buf = torch.zeros(nw * 8, dtype=torch.int32, device=seeds.device)
+    buf = torch.zeros(nw * 16, dtype=torch.int32, device=seeds.device)
     rtamd.check(L.spt_trace_set(C.c_void_p(buf.data_ptr())))
     rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
                                          seeds.data_ptr(), px.data_ptr(), W, H, r0, r1, 0, SPP, 0, None,
                                          st.cuda_stream))
     torch.cuda.synchronize()
     rtamd.check(L.spt_trace_set(None))
-    t = buf.cpu().numpy().view(np.uint32).reshape(nw, 8).astype(np.int64)
+    t = buf.cpu().numpy().view(np.uint32).reshape(nw, 16).astype(np.int64)
     return t, gx, gy
 
 
