@@ -380,6 +380,35 @@ def cornell_line(args, dev, w, h, spp, workload):
             "Msamples_per_s": round(w * h * spp / ms / 1e3, 2), "rays_per_frame": rays}
 
 
+def collective_name():
+    """What carries the HDR all-gather at N > 1: RCCL (torch's "nccl" backend
+    on ROCm) unless the one-GPU rehearsal knob RT_BENCH_BACKEND picked gloo."""
+    return "RCCL" if os.environ.get("RT_BENCH_BACKEND", "nccl") == "nccl" else "gloo"
+
+
+def dropin_line(args):
+    """Side line: the reference's own host path over the drop-in --
+    displayfunc.cpp's idle loop calling UpdateRenderingGPU (csrc/shim_smallpt.cpp
+    in place of smallptGPU.cpp) on the Cornell frame at 1920x1080: 20 single
+    passes, then time-boxed calls (smallptGPU.cpp:739-755) for ~3 s each way,
+    samples/s as the reference's caption computes it (:777-781).  "batched":
+    the shim's time box launches batches of passes (one wait per batch; the
+    same per-pixel sample sequence); "per_pass": one launch and one wait per
+    pass, as smallptGPU.cpp does (RT_SPT_SHIM_BATCH=1)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "native", "smallpt_dropin_bench")
+    if not os.access(exe, os.X_OK):
+        return {"skipped": "tests/native/smallpt_dropin_bench not built"}
+    out = {"workload": "smallpt drop-in (shim_smallpt.cpp UpdateRenderingGPU), Cornell 1920x1080, "
+                       "20 single passes then time-boxed calls"}
+    for tag, env in (("batched", {}), ("per_pass", {"RT_SPT_SHIM_BATCH": "1"})):
+        r = subprocess.run([exe, str(W), str(H), "3.0"], capture_output=True, text=True, timeout=120,
+                           env=dict(os.environ, **env))
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        out[tag] = json.loads(line[-1]) if r.returncode == 0 and line else {"error": r.stderr[-300:]}
+    return out
+
+
 def tiled_line(step, cnt, dev, world, distributed, workload, spp, frames=2, **scene):
     """A frame of `workload` tiled across the job's GPUs exactly as the
     headline steps are (each rank renders its rows, then the RCCL all-gather
@@ -408,7 +437,8 @@ def tiled_line(step, cnt, dev, world, distributed, workload, spp, frames=2, **sc
         el = t.item()
     ms = el * 1e3 / frames
     rays = counts[0] + counts[1]
-    return {"workload": "%s, tiled across %d GPU(s)%s" % (workload, world, " + RCCL HDR all-gather" if world > 1 else ""),
+    return {"workload": "%s, tiled across %d GPU(s)%s" % (
+                workload, world, " + %s HDR all-gather" % collective_name() if world > 1 else ""),
             "n_gpus": world, "ms_per_frame": round(ms, 3), "Mrays_per_s": round(rays / ms / 1e3, 2),
             "Msamples_per_s": round(W * H * spp / ms / 1e3, 2), "rays_per_frame": rays}
 
@@ -470,6 +500,8 @@ def main():
     freed = [None] * nbuf        # event: buffer b's last gather finished
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
+    gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]          # each timed step's all-gather + repack (gather stream)
     nframe = [0]
 
     def step(i=None, counters=None, spp=SPP, sc=None, cm=None):
@@ -496,7 +528,11 @@ def main():
         if world > 1:            # RCCL all-gather of the HDR bands + RGBA8 repack
             gs.wait_stream(s)
             with torch.cuda.stream(gs):
+                if i is not None:
+                    gev[i][0].record(gs)
                 gathers[b].gather()
+                if i is not None:
+                    gev[i][1].record(gs)
             if pipelined:
                 freed[b] = torch.cuda.Event()
                 freed[b].record(gs)
@@ -523,7 +559,17 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    ranks = None
     if distributed:
+        # Per-rank view of the timed steps (HIP events): render kernel ms,
+        # all-gather + repack ms on the gather stream, and this rank's wall
+        # clock -- gathered so rank 0 can say which rank and which phase set
+        # the frame time.
+        gather_ms = float(np.mean([a.elapsed_time(b) for a, b in gev]))
+        mine = torch.tensor([kern_ms, gather_ms, elapsed * 1e3 / args.steps], dtype=torch.float64, device=dev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        ranks = [r.tolist() for r in allr]
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = t.tolist()
@@ -552,8 +598,8 @@ def main():
         "data": "synthetic: reference Cornell scene (scene.h:29-40), glibc rand() seeds, random-free camera",
         "config": {"workload": "smallpt Cornell 1920x1080 64spp RadiancePathTracing, one frame per step",
                    "frame": [W, H], "spp": SPP, "spheres": ns, "rows_per_gpu": B,
-                   "parallelism": ("%s x%d + RCCL HDR all-gather%s" % (
-                       "interleaved 8-row groups" if interleaved else "row bands", world,
+                   "parallelism": ("%s x%d + %s HDR all-gather%s" % (
+                       "interleaved 8-row groups" if interleaved else "row bands", world, collective_name(),
                        " (pipelined)" if pipelined else "")) if world > 1 else "single GPU"},
         "frames_per_s": round(1e3 / ms_per_step, 3),
         "Msamples_per_s": round(W * H * SPP / (ms_per_step * 1e-3) / 1e6, 2),
@@ -576,6 +622,19 @@ def main():
                                 "kernel time), from the PMC digest"},
     }
     if distributed:
+        # Where the N-GPU frame time goes: with pipelining a step costs the
+        # slowest rank's render when the gather hides behind the next frame's
+        # render (overlap 1), render + gather when nothing overlaps (0).
+        rmax = max(r[0] for r in ranks)
+        gmax = max(r[1] for r in ranks)
+        out["ranks"] = {"render_ms": [round(r[0], 3) for r in ranks],
+                        "gather_ms": [round(r[1], 3) for r in ranks],
+                        "wall_ms_per_step": [round(r[2], 3) for r in ranks],
+                        "collective": collective_name(),
+                        "overlap": round(min(1.0, max(0.0, (rmax + gmax - ms_per_step) / gmax)), 3) if gmax > 0 else None,
+                        "note": "render_ms / gather_ms: mean over the timed steps of HIP events around the render "
+                                "launch (render stream) and the HDR all-gather + RGBA8 repack (gather stream); "
+                                "overlap = (max render + max gather - ms_per_step) / max gather"}
         # Self-check of the sharded path (outside the timed region): the last
         # assembled frame must equal one GPU rendering the whole frame.
         last = (nframe[0] - 1) % nbuf
@@ -606,6 +665,7 @@ def main():
             out["queue3203"] = queue_line(args, dev)
             if not args.no_cornell_extra:
                 out["configs2"] = cornell_line(args, dev, 1024, 768, 64, "configs[2]: Cornell 1024x768, 64 spp, 1 GPU")
+                out["dropin"] = dropin_line(args)
             if not args.no_cpu:
                 out["configs0"] = configs0_line(args, dev)
         out["cpu_baseline"] = None if args.no_cpu else cpu_baseline(args)

@@ -246,11 +246,16 @@ int spt_multi_band_buffers(const spt_multi *m, int k, int *device, float **d_col
 /* spt_render over several GPUs (SURVEY.md §8(b) "spt_render(..., ngpus)"):
  * the same contract and results as spt_render, the frame tiled in row bands
  * over devices[0..ngpus-1] (NULL: 0..ngpus-1), host buffers assembled band
- * by band.  Blocking. */
+ * by band.  Blocking.  The band context (per band: scene, buffers, stream)
+ * is kept across calls: the same devices and frame size reuse it, a changed
+ * sphere array re-prepares only the scenes; rt_release frees it. */
 int spt_render_multi(const rt_sphere *spheres, unsigned nspheres, const rt_camera *camera,
                      float *colors, uint32_t *seeds, uint32_t *pixels, int w, int h,
                      int first_sample, int nsamples, int mode, uint64_t *counters,
                      const int *devices, int ngpus);
+/* Diagnostics of spt_render_multi's cached context: out[0] = band contexts
+ * built, out[1] = scene preparations (both since the process started). */
+int spt_multi_cache_info(uint64_t *out);
 
 /* ------------------------------------------------------------ queue tracer (3.2.03) */
 /* Blocking, host buffers, whole frame: raytracer_non_kernel(pixels, w, h,

@@ -204,6 +204,7 @@ extern "C" int rt_set_device(int device)
 
 extern "C" int rt_release(void)
 {
+    rtrt::release_cached_multi();
     rtrt::release_cached_scenes();        // under each device state's lock
     std::lock_guard<std::mutex> lk(rtrt::g_mu);
     for (int d = 0; d < 64; d++) {

@@ -67,6 +67,8 @@ double pool_fraction(DeviceState &st, int which, long long trees, double initial
 // Frees the per-device scenes cached by spt_render / spt_render_async
 // (smallpt.hip; rt_release).
 void release_cached_scenes();
+// Frees spt_render_multi's cached band context (spt_multi.hip; rt_release).
+void release_cached_multi();
 // The calling thread's rt_set_device choice (-1: none, HIP's current device).
 int thread_device();
 // Saves the calling thread's device selection (rt_set_device and HIP's

@@ -115,10 +115,13 @@ void AllocateBuffers()
 }
 
 // ExecuteKernel (smallptGPU.cpp:617-640): one pass = one sample per pixel,
-// every band on its own device.
-void ExecuteKernel()
+// every band on its own device; passes > 1 runs that many consecutive passes
+// in one launch (samples currentSample .. currentSample + passes - 1, the
+// same results as one launch per pass: the kernel keeps each pixel's
+// sample order).
+void ExecuteKernel(int passes = 1)
 {
-    int rc = spt_multi_render_async(frame, &camera, currentSample, 1, smallptHipMode, 0);
+    int rc = spt_multi_render_async(frame, &camera, currentSample, passes, smallptHipMode, 0);
     if (rc) die("Failed to enqueue HIP work", rc);
 }
 
@@ -143,6 +146,12 @@ void SetUpHIP()
 // UpdateRenderingGPU (smallptGPU.cpp:642-782): a single pass for the first
 // 20 samples, then passes until 0.5 * min(currentSample - 20, 100) / 100 s
 // have elapsed; then the blocking read of the RGBA8 frame and the caption.
+// The reference launches and waits for (clFinish) every pass of the time
+// box; here a launch runs a batch of passes sized from the measured pass
+// time to about an eighth of the time left (at least one pass), so the
+// kernel keeps a pixel's samples in-lane and the host waits once per batch
+// -- the same sample sequence per pixel, the box overshot by at most a
+// batch.  RT_SPT_SHIM_BATCH=1: one pass per launch, as the reference.
 void UpdateRenderingGPU()
 {
     double startTime = WallClockTime();
@@ -154,12 +163,21 @@ void UpdateRenderingGPU()
         const int c = currentSample - 20;
         const float k = (c < 100 ? c : 100) / 100.f;
         const float tresholdTime = 0.5f * k;
+        const char *be = getenv("RT_SPT_SHIM_BATCH");
+        const int max_batch = be && atoi(be) > 0 ? atoi(be) : 256;
+        int batch = 1;
         for (;;) {
-            ExecuteKernel();
+            const double t0 = WallClockTime();
+            ExecuteKernel(batch);
             Finish();
-            currentSample++;
-            const float elapsedTime = WallClockTime() - startTime;
+            currentSample += batch;
+            const double now = WallClockTime();
+            const float elapsedTime = now - startTime;
             if (elapsedTime > tresholdTime) break;
+            const double per_pass = (now - t0) / batch;
+            const double left = tresholdTime - elapsedTime;
+            int next = per_pass > 0 ? (int)(left / per_pass / 8.0) : 1;
+            batch = next < 1 ? 1 : (next > max_batch ? max_batch : next);
         }
     }
     int rc = spt_multi_download(frame, nullptr, nullptr, pixels);   // every band's rows

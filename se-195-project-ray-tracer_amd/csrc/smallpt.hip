@@ -257,6 +257,8 @@ struct BvhView {
     const int *aid;
     int nalways, nnodes;
     const uint4 *wnode;   // the 8-wide layout (spt_bvh.h WideBuild: 7 x 16 B per node), staged in LDS
+    const uint4 *wmax;    //   per node and slot the highest reference index below (2 x 16 B per node;
+                          //   staged by the counted kernels only)
     int wnodes, wdepth;   //   its node count and depth (levels of wide nodes)
 };
 constexpr float BVH_ALPHA_R = 1.f / 64.f;   // per node, with BETA, in the node record
@@ -319,7 +321,8 @@ struct BvhWalk {
     float t;
     int id, node, pend;
     unsigned m;             // 8-wide walk: node = the current node (-1: root not yet visited), m = its
-    int sp;                 //   children still to visit (visit order), sp = stacked (node, mask) entries
+    int sp, bpos;           //   children still to visit (visit order), sp = stacked (node, mask) entries,
+                            //   bpos = hierarchy position of the best leaf hit so far (-1: none)
 #if RT_BVH_PEND2
     int pend2;              // a second crossed leaf (only while pend holds one)
 #endif
@@ -590,8 +593,11 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
 // slack.  Visit order: the child in slot p ^ octant at position p (the host
 // put each octant's front child in the slot of that octant); the per-lane
 // stack holds (node << 8 | remaining mask) entries in LDS, one per level.
+// idmin >= 0 (the counted any-hit): only children holding a reference index
+// above idmin (hid: the node's eight highest-index words) are crossed.
 __device__ __forceinline__ unsigned wide_visit(const uint4 *__restrict__ N, const ray3 &r, float ix, float iy,
-                                               float iz, float alpha, int oct, float lim)
+                                               float iz, float alpha, int oct, float lim,
+                                               const unsigned *__restrict__ hid = nullptr, int idmin = -1)
 {
     const uint4 h0 = N[0];
     const float2 h1 = *(const float2 *)(N + 1);
@@ -605,7 +611,11 @@ __device__ __forceinline__ unsigned wide_visit(const uint4 *__restrict__ N, cons
     const float bx = cx * ix, by = cy * iy, bz = cz * iz;
     const float mx = m * fabsf(ix), my = m * fabsf(iy), mz = m * fabsf(iz);
     const float bnx = bx - mx, bfx = bx + mx, bny = by - my, bfy = by + my, bnz = bz - mz, bfz = bz + mz;
-    const unsigned valid = h0.w >> 24;
+    unsigned valid = h0.w >> 24;
+    if (hid && idmin >= 0) {
+#pragma unroll
+        for (int sl = 0; sl < 8; sl++) valid &= ((int)hid[sl] > idmin ? 1u : 0u) << sl | ~(1u << sl);
+    }
     // The child boxes, a half (four slots) at a time: words 16 + 6 h ..
     // 21 + 6 h hold lo_x, lo_y, lo_z, hi_x, hi_y, hi_z of slots 4h .. 4h+3.
     // The near plane of an axis is the low byte for a positive direction.
@@ -638,6 +648,9 @@ __device__ __forceinline__ unsigned wide_visit(const uint4 *__restrict__ N, cons
 #ifndef RT_WIDE_BUDGET
 #define RT_WIDE_BUDGET 16   // wide-walk trips per render-loop iteration before a lane's query is suspended
 #endif
+#ifndef RT_WIDE_STOP
+#define RT_WIDE_STOP 32     // wide walk: end the call once <= STOP/64 of its lanes still walk (configs[4] 36.3 -> 29.0 ms)
+#endif
 constexpr int WIDE_WORDS = 28;   // per node (spt_bvh.h)
 
 template <bool COUNT>
@@ -645,6 +658,7 @@ __device__ __forceinline__ void wide_begin(const BvhView &B, const ray3 &r, bool
 {
     bvh_begin<COUNT>(B, r, shadow, t, W);
     W.node = -1;                                        // the root is visited by the first trip
+    W.bpos = -1;
     W.m = (!COUNT && shadow && W.id >= 0) ? 0u : 1u;
     W.sp = 0;
 }
@@ -655,13 +669,22 @@ __device__ __forceinline__ void wide_begin(const BvhView &B, const ray3 &r, bool
 // stk[64 k + l]).  Crossed leaves are postponed and tested together as in
 // bvh_walk (two pending per lane); a leaf of more than four spheres is tested
 // four at a time.
+// opts: trip budget per call (bits 8..15), leaf batch threshold in 1/64 of
+// the walking lanes (16..23), early stop (24..31): the call ends once at most
+// stop/64 of the lanes that entered it are still walking (64: never).
 template <bool COUNT>
 __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigned *__restrict__ stk, const ray3 &r,
-                          bool shadow, BvhWalk &W)
+                          bool shadow, BvhWalk &W, int opts)
 {
+    const int budget = (opts >> 8) & 255, batch = (opts >> 16) & 255, stop = (opts >> 24) & 255;
     const float maxt = W.t;
     float t = W.t;
-    int id = W.id, cur = W.node, pend = W.pend, pend2 = W.pend2, sp = W.sp;
+    // The best leaf hit so far is kept as its hierarchy position (bpos) and
+    // its reference index loaded once, when the query completes -- not after
+    // every leaf pass (a dependent global load: ~1/3 of a lone wave's leaf
+    // pass, tools/c5_phase.py).  Ties and the counted any-hit's highest
+    // occluder still load indices on the spot.
+    int id = W.id, cur = W.node, pend = W.pend, pend2 = W.pend2, sp = W.sp, bpos = W.bpos;
     unsigned m = W.m;
     const float dx = fabsf(r.d.x) < 1e-30f ? copysignf(1e-30f, r.d.x) : r.d.x;
     const float dy = fabsf(r.d.y) < 1e-30f ? copysignf(1e-30f, r.d.y) : r.d.y;
@@ -671,7 +694,9 @@ __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigne
     const float alpha = e < 0x1p-16f ? BVH_K * (1.04e-3f + __builtin_amdgcn_sqrtf(e + 0x1p-22f)) : 1e30f;
     const int oct = (dx < 0.f ? 1 : 0) | (dy < 0.f ? 2 : 0) | (dz < 0.f ? 4 : 0);
     const unsigned *Lw = (const unsigned *)L;
+    const unsigned *Lmax = COUNT ? (const unsigned *)(L + 7 * B.wnodes) : nullptr;   // (counted kernels)
     unsigned *my = stk + (threadIdx.x & 63);
+    const int n0 = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true));   // lanes in this call
     int trips = 0;
     while (true) {
         if (m != 0 && pend2 == 0) {
@@ -688,7 +713,10 @@ __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigne
                 if (pend == 0) pend = ~cw;
                 else pend2 = ~cw;
             } else {
-                const unsigned hm = wide_visit(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t);
+                const unsigned hm =
+                    COUNT ? wide_visit(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t,
+                                       Lmax + 8 * cw, shadow ? id : -1)
+                          : wide_visit(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t);
                 if (hm) {
                     if (m) {
                         my[64 * sp] = ((unsigned)cur << 8) | m;
@@ -708,13 +736,17 @@ __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigne
         trips++;
         const unsigned long long pm = __builtin_amdgcn_ballot_w64(pend != 0);
         const unsigned long long sm = __builtin_amdgcn_ballot_w64(m != 0 && pend2 == 0);
+        const bool out = trips >= budget || 64 * __builtin_popcountll(pm | sm) <= stop * n0;
         if (pm == 0) {
-            if (sm == 0 || trips >= RT_WIDE_BUDGET) break;
+            if (sm == 0 || out) break;
             continue;
         }
-        if (sm != 0 && trips < RT_WIDE_BUDGET &&
-            64 * __builtin_popcountll(pm & ~sm) < RT_BVH_BATCH * __builtin_popcountll(pm | sm))
+        if (sm != 0 && !out && 64 * __builtin_popcountll(pm & ~sm) < batch * __builtin_popcountll(pm | sm))
             continue;
+#ifdef RT_SPT_TRACE
+        const unsigned long long tr_l0 = __builtin_amdgcn_s_memtime();
+        W.tr_leafruns++;
+#endif
         if (pend != 0) {
             const int f = pend & 0xffffff, c = pend >> 24, c4 = c < BVH_LEAF_MAX ? c : BVH_LEAF_MAX;
             float4 g[BVH_LEAF_MAX];
@@ -737,7 +769,6 @@ __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigne
 #pragma unroll
                 for (int q = 0; q < BVH_LEAF_MAX; q++) dq[q] = sphere_hit(g[q], r);
             }
-            int bpos = -1;
 #pragma unroll
             for (int q = 0; q < BVH_LEAF_MAX; q++) {
                 if (q < c4) {
@@ -760,29 +791,38 @@ __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigne
                     }
                 }
             }
-            if (bpos >= 0) id = B.id[bpos];
             if (c > BVH_LEAF_MAX) {
                 pend = (f + BVH_LEAF_MAX) | ((c - BVH_LEAF_MAX) << 24);
             } else {
                 pend = pend2;
                 pend2 = 0;
             }
-            if (!COUNT && shadow && id >= 0) {
+            if (!COUNT && shadow && (id >= 0 || bpos >= 0)) {
                 m = 0;
                 sp = 0;
                 pend = pend2 = 0;
             }
         }
-        if (trips >= RT_WIDE_BUDGET) break;
+#ifdef RT_SPT_TRACE
+        W.tr_leaf += (unsigned)(__builtin_amdgcn_s_memtime() - tr_l0);
+#endif
+        if (out) break;
     }
+#ifdef RT_SPT_TRACE
+    W.tr_trips += trips;
+#endif
+    const bool done = m == 0 && pend == 0;
+    // (an uncounted any-hit only needs "some occluder": no index load)
+    if (done && bpos >= 0) id = (!COUNT && shadow) ? 0x7fffffff : B.id[bpos];
     W.t = t;
     W.id = id;
+    W.bpos = bpos;
     W.node = cur;
     W.m = m;
     W.sp = sp;
     W.pend = pend;
     W.pend2 = pend2;
-    return m == 0 && pend == 0;
+    return done;
 }
 
 struct Counts { unsigned long long isect, isectp, tests, samples; };
@@ -878,7 +918,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
               int prio_sched, const int *__restrict__ group_order, unsigned *__restrict__ group_cost,
               const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
               const float4 *__restrict__ g_col, const float4 *__restrict__ g_lrec, int nlights,
-              BvhView bvh, unsigned long long *__restrict__ counters, int *__restrict__ work)
+              BvhView bvh, unsigned long long *__restrict__ counters, int *__restrict__ work, int split)
 {
     constexpr bool LDS = GEO == GEO_LDS;
     // GEO_WIDE: persistent waves -- each wave takes 8x8 tiles from a work
@@ -909,7 +949,10 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     if (GEO == GEO_WIDE) {
         uint4 *d = (uint4 *)smem;
         for (int i = threadIdx.x; i < 7 * bvh.wnodes; i += blockDim.x) d[i] = bvh.wnode[i];
-        wstk = (unsigned *)(smem + (size_t)112 * bvh.wnodes) + (size_t)(threadIdx.x >> 6) * 64 * (bvh.wdepth - 1);
+        if (COUNT)
+            for (int i = threadIdx.x; i < 2 * bvh.wnodes; i += blockDim.x) d[7 * bvh.wnodes + i] = bvh.wmax[i];
+        wstk = (unsigned *)(smem + (size_t)(COUNT ? 144 : 112) * bvh.wnodes) +
+               (size_t)(threadIdx.x >> 6) * 64 * (bvh.wdepth - 1);
         __syncthreads();
     }
 
@@ -931,8 +974,11 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     unsigned prof_l[PB_N] = {}, prof_w[PB_N] = {};
 #endif
     // Work item f: tile (f & 3) of dispatch slot f >> 2.  Static launches: one
-    // item per wave, slot (wave >> 2) * gridDim.x + blockIdx.x.
-    const int nwork = 4 * ((ntiles + 3) >> 2);
+    // item per wave, slot (wave >> 2) * gridDim.x + blockIdx.x.  Persistent
+    // launches may split every tile over 2^split items of 64 >> split pixels
+    // (lanes beyond them idle): a tile's pixels then run on several SIMDs.
+    // (split: bits 0..1; the wide walk's options above them, wide_walk)
+    const int nwork = (4 * ((ntiles + 3) >> 2)) << (PERSIST ? (split & 3) : 0);
     int f = ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) * 4 + (wave & 3);
     if (PERSIST) {
         int v = 0;
@@ -940,9 +986,12 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         f = __shfl(v, 0, 64);
     }
     while (!PERSIST || f < nwork) {
-    const int slot = f >> 2;
+    const int sp_ = PERSIST ? (split & 3) : 0;
+    const int item = f >> sp_, sub = f & ((1 << sp_) - 1);
+    const int slot = item >> 2;
     const int grp = (SCHED && group_order) ? group_order[slot] : slot;
-    const int tile = grp * 4 + (f & 3);
+    const int tile = grp * 4 + (item & 3);
+    const int li = (sub << (6 - sp_)) + lane;           // pixel of the 8x8 tile (valid: lane < 64 >> split)
     unsigned long long t_start = 0;
     if (SCHED) t_start = __builtin_amdgcn_s_memrealtime();
     // GSTORE (hierarchy kernels): per group of the block a 32x8 staging
@@ -954,17 +1003,18 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         if ((threadIdx.x & 255) == 0) *(int *)(GS_BASE() + 6144) = 0;
         __syncthreads();
     }
-    const int x = (tile % tiles_x) * 8 + (lane & 7);
+    const int x = (tile % tiles_x) * 8 + (li & 7);
     // gstride > 1: the window is every gstride-th 8-row group from row_begin
     // (spt_scene_render_groups_async, multi-GPU load balance).
-    const int y = row_begin + (tile / tiles_x) * 8 * gstride + (lane >> 3);
+    const int y = row_begin + (tile / tiles_x) * 8 * gstride + (li >> 3);
 #ifdef RT_SPT_TRACE
-    const bool active = tile < ntiles && x < w && y < row_end && (g_spt_only_group < 0 || grp == g_spt_only_group);
+    const bool active = lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end &&
+                        (g_spt_only_group < 0 || grp == g_spt_only_group);
     unsigned tr_walk = 0, tr_leaf = 0, tr_trips = 0, tr_leafruns = 0, tr_queries = 0;
     const unsigned long long tr_c0 = __builtin_amdgcn_s_memtime();
     const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();
 #else
-    const bool active = tile < ntiles && x < w && y < row_end;
+    const bool active = lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end;
 #endif
 
 #ifdef RT_SPT_TRACE
@@ -1147,7 +1197,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 tr_queries += !walking;
 #endif
                 if (!walking) wide_begin<COUNT>(bvh, ray, shadow, t, walk);
-                walking = !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk);
+                walking = !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
 #ifdef RT_SPT_TRACE
                 tr_walk += (unsigned)(__builtin_amdgcn_s_memtime() - tr_w0);
 #endif
@@ -1406,7 +1456,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             seeds_out[2 * (size_t)i + 1] = s1;
         }
 #ifdef RT_SPT_TRACE
-        if (GEO == GEO_BVH) {
+        if (GEO == GEO_BVH || GEO == GEO_WIDE) {
             tr_leaf = walk.tr_leaf;
             tr_trips = walk.tr_trips;
             tr_leafruns = walk.tr_leafruns;
@@ -1587,9 +1637,9 @@ int wide_wpb()
     const int v = e ? atoi(e) : WIDE_WPB;
     return v >= 1 && v <= 16 ? v : WIDE_WPB;
 }
-size_t wide_lds_bytes(int wnodes, int wdepth, int wpb)
+size_t wide_lds_bytes(int wnodes, int wdepth, int wpb, bool counted = true)
 {
-    return (size_t)112 * wnodes + (size_t)wpb * 256 * (wdepth > 1 ? wdepth - 1 : 1);
+    return (size_t)(counted ? 144 : 112) * wnodes + (size_t)wpb * 256 * (wdepth > 1 ? wdepth - 1 : 1);
 }
 }  // namespace
 
@@ -1668,13 +1718,21 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     if (g.wpb == 16 && lds < 81 * 1024) lds = 81 * 1024;   // > half the CU's 160 KiB: one block per CU
     int *work = nullptr;
     if (GEO == rt::smallpt::GEO_WIDE) {
-        lds = wide_lds_bytes(sc.bvh.wnodes, sc.bvh.wdepth, g.wpb);
+        lds = wide_lds_bytes(sc.bvh.wnodes, sc.bvh.wdepth, g.wpb, COUNT);
         work = sc.d_work + (sc.work_next++ % spt_scene::NWORK);
         if (hipMemsetAsync(work, 0, sizeof(int), s) != hipSuccess) return;   // (check_launch reports it)
     }
+    int split = 0;
+    if (GEO == rt::smallpt::GEO_WIDE) {
+        int sp = 0, budget = RT_WIDE_BUDGET, batch = RT_BVH_BATCH, stop = RT_WIDE_STOP;
+        if (const char *e = getenv("RT_SPT_SPLIT")) sp = std::min(std::max(atoi(e), 0), 3);   // tools: tiles split 2^k ways
+        if (const char *e = getenv("RT_WIDE_OPTS")) sscanf(e, "%d,%d,%d", &budget, &batch, &stop);   // tools: A/B
+        split = (RT_WIDE_PERSIST ? sp : 0) | (std::min(std::max(budget, 1), 255) << 8) |
+                (std::min(std::max(batch, 0), 64) << 16) | (std::min(std::max(stop, 0), 64) << 24);
+    }
     hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.gstride, first,
-                       ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt, work);
+                       ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt, work, split);
 }
 
 template <int GEO>
@@ -1743,14 +1801,17 @@ int build_scene_bvh(spt_scene *sc, const rt_sphere *spheres)
         ids[j] = i;
     }
     const size_t nb_bytes = sizeof(float4) * nodes.size(), g_bytes = sizeof(float4) * geo.size(),
-                 i_bytes = sizeof(int) * ids.size(), w_bytes = wide ? 4 * wb.words.size() : 0;
+                 i_bytes = sizeof(int) * ids.size(), w_bytes = wide ? 4 * wb.words.size() : 0,
+                 m_bytes = wide ? 4 * wb.maxid.size() : 0;
     const size_t w_off = (nb_bytes + g_bytes + i_bytes + 15) & ~(size_t)15;
-    hipError_t e = hipMalloc(&sc->d_bvh, w_off + w_bytes + 16);
+    hipError_t e = hipMalloc(&sc->d_bvh, w_off + w_bytes + m_bytes + 16);
     char *base = (char *)sc->d_bvh;
     if (e == hipSuccess) e = hipMemcpy(base, nodes.data(), nb_bytes, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(base + nb_bytes, geo.data(), g_bytes, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(base + nb_bytes + g_bytes, ids.data(), i_bytes, hipMemcpyHostToDevice);
     if (e == hipSuccess && wide) e = hipMemcpy(base + w_off, wb.words.data(), w_bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && wide)
+        e = hipMemcpy(base + w_off + w_bytes, wb.maxid.data(), m_bytes, hipMemcpyHostToDevice);
     if (e == hipSuccess && wide) e = hipMalloc(&sc->d_work, sizeof(int) * spt_scene::NWORK);
     if (e != hipSuccess) return rtrt::fail_hip(e, "spt_scene_create hierarchy upload");
     rt::smallpt::BvhView &v = sc->bvh;
@@ -1762,6 +1823,7 @@ int build_scene_bvh(spt_scene *sc, const rt_sphere *spheres)
     v.nalways = na;
     v.nnodes = nn;
     v.wnode = wide ? (const uint4 *)(base + w_off) : nullptr;
+    v.wmax = wide ? (const uint4 *)(base + w_off + w_bytes) : nullptr;
     v.wnodes = wide ? wb.nnodes : 0;
     v.wdepth = wide ? wb.depth : 0;
     return RT_OK;

@@ -8,7 +8,7 @@
 // geomfunc.h:71-110).  A hierarchy only skips spheres whose float
 // SphereIntersect distance provably cannot be taken; smallpt.hip's "Skipping
 // rule" comment gives the margin argument.  Two layouts are built:
-//   * BvhBuild: binned-SAH binary tree, leaves of <= 4 spheres, eight
+//   * BvhBuild: binned-SAH binary tree (64 bins), leaves of <= 4 spheres, eight
 //     depth-first layouts (one per ray-direction octant, near child first)
 //     with escape links -- walked stacklessly from global memory;
 //   * WideBuild: the same tree collapsed to 8 children per node, child boxes
@@ -34,6 +34,9 @@ constexpr float ALPHA_R = 1.f / 64.f;   // margin per unit of a box's half diago
 constexpr int LEAF = 4;                  // spheres per leaf
 constexpr int MIN_SPHERES = 256;         // scenes below this are scanned in full
 constexpr int MAX_ALWAYS = 16;           // spheres tested outside the hierarchy (radius > 64 x median)
+#ifndef SPT_SAH_BINS
+#define SPT_SAH_BINS 64   // binned-SAH bins per axis (16: configs[4] heavy-tile rays visit ~20 % more nodes)
+#endif
 
 struct HostNode {
     float lo[3], hi[3];
@@ -94,8 +97,8 @@ struct BvhBuild {
             nodes[me] = nd;
             return me;
         }
-        // SAH over 16 centroid bins per axis.
-        constexpr int NB = 16;
+        // SAH over SPT_SAH_BINS centroid bins per axis.
+        constexpr int NB = SPT_SAH_BINS;
         int best_ax = -1, best_b = 0;
         float best_cost = 1e30f;
         for (int ax = 0; ax < 3; ax++) {
@@ -226,11 +229,24 @@ struct WideBuild {
     std::vector<uint32_t> words;
     int nnodes = 0, depth = 0;          // depth: levels of wide nodes (the stack needs depth - 1 entries)
     int leaf_max = LEAF;                // binary subtrees of <= leaf_max spheres become one leaf child
-    std::vector<int> cnt;               // spheres under each binary node
+    // Per node and slot the highest reference index under that child (8
+    // words per node, 0 for empty slots): the counted any-hit walk, which
+    // must find the highest occluder (IntersectP's early-exit position),
+    // skips children that cannot hold a higher one.
+    std::vector<uint32_t> maxid;
+    std::vector<int> cnt, mx;           // spheres / highest reference index under each binary node
     int count(const BvhBuild &b, int r)
     {
         const HostNode &h = b.nodes[r];
-        return cnt[r] = h.left < 0 ? h.count : count(b, h.left) + count(b, h.right);
+        if (h.left < 0) {
+            int m = -1;
+            for (int j = 0; j < h.count; j++) m = std::max(m, b.idx[h.first + j]);
+            mx[r] = m;
+            return cnt[r] = h.count;
+        }
+        const int c = count(b, h.left) + count(b, h.right);
+        mx[r] = std::max(mx[h.left], mx[h.right]);
+        return cnt[r] = c;
     }
     bool is_leaf(const BvhBuild &b, int r) const { return b.nodes[r].left < 0 || cnt[r] <= leaf_max; }
     int first(const BvhBuild &b, int r) const { return b.nodes[r].left < 0 ? b.nodes[r].first : first(b, b.nodes[r].left); }
@@ -266,6 +282,7 @@ struct WideBuild {
         depth = std::max(depth, level + 1);
         const int me = nnodes++;
         words.resize((size_t)nnodes * WIDE_WORDS, 0u);
+        maxid.resize((size_t)nnodes * WIDE, 0u);
         std::vector<int> kids;
         collapse(b, r, kids);
         const int nk = (int)kids.size();
@@ -347,14 +364,18 @@ struct WideBuild {
         for (int s = 0; s < WIDE; s++) w[8 + s] = (uint32_t)child[s];
         for (int a = 0; a < 6; a++)
             for (int s = 0; s < WIDE; s++) w[16 + 6 * (s >> 2) + a] |= (uint32_t)q[a][s] << (8 * (s & 3));
+        for (int s = 0; s < WIDE; s++)
+            if (child_in[s] >= 0) maxid[(size_t)me * WIDE + s] = (uint32_t)mx[kids[child_in[s]]];
         return me;
     }
 
     void build(const BvhBuild &b)
     {
         words.clear();
+        maxid.clear();
         nnodes = depth = 0;
         cnt.assign(b.nodes.size(), 0);
+        mx.assign(b.nodes.size(), -1);
         if (!b.nodes.empty()) {
             count(b, 0);
             emit(b, 0, 0);

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <stdlib.h>
 #include <string.h>
+#include <string>
 #include <vector>
 #include "rt_runtime.h"
 #include <rccl/rccl.h>
@@ -419,20 +420,94 @@ extern "C" int spt_multi_band_buffers(const spt_multi *m, int k, int *device, fl
     return RT_OK;
 }
 
+namespace {
+// spt_render_multi's band context, kept across calls as spt_render keeps its
+// scene (smallptGPU.cpp:100-167,209-615 create the buffers once and reuse
+// them every pass): the same devices and frame size reuse every band's
+// buffers, stream and scene; a changed sphere array (compared byte for byte)
+// re-prepares only the scenes; anything else builds a new context.
+struct MultiCache {
+    std::vector<int> devices;
+    int w = 0, h = 0;
+    std::vector<rt_sphere> host;
+    std::string hooks;                 // the scenes' preparation hooks (spt_scene_create's getenv)
+    spt_multi *m = nullptr;
+    unsigned long long contexts = 0, preps = 0;
+};
+MultiCache g_multi_cache;
+std::mutex g_multi_mu;
+
+std::string multi_hooks()
+{
+    const char *a = getenv("RT_SPT_NO_BVH"), *b = getenv("RT_SPT_GEO"), *c = getenv("RT_SPT_WIDE");
+    return std::string(a ? "1" : "0") + "|" + (b ? b : "") + "|" + (c ? c : "");
+}
+}  // namespace
+
+namespace rtrt {
+void release_cached_multi()
+{
+    std::lock_guard<std::mutex> lk(g_multi_mu);
+    destroy_multi(g_multi_cache.m);
+    g_multi_cache.m = nullptr;
+    g_multi_cache.host.clear();
+    g_multi_cache.devices.clear();
+}
+}  // namespace rtrt
+
+extern "C" int spt_multi_cache_info(uint64_t *out)
+{
+    if (!out) return rtrt::fail(RT_ERR_INVALID, "spt_multi_cache_info: null pointer");
+    std::lock_guard<std::mutex> lk(g_multi_mu);
+    out[0] = g_multi_cache.contexts;
+    out[1] = g_multi_cache.preps;
+    return RT_OK;
+}
+
 extern "C" int spt_render_multi(const rt_sphere *spheres, unsigned nspheres, const rt_camera *camera,
                                 float *colors, uint32_t *seeds, uint32_t *pixels, int w, int h, int first_sample,
                                 int nsamples, int mode, uint64_t *counters, const int *devices, int ngpus)
 {
     if (!spheres || !camera || !colors || !seeds || !pixels || w < 1 || h < 1 || nspheres < 1 ||
-        first_sample < 0 || nsamples < 0)
+        first_sample < 0 || nsamples < 0 || ngpus < 1 || ngpus > 64)
         return rtrt::fail(RT_ERR_INVALID, "spt_render_multi: bad arguments");
-    spt_multi *m;
-    int rc = spt_multi_create(spheres, nspheres, w, h, devices, ngpus, &m);
-    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(g_multi_mu);
+    MultiCache &c = g_multi_cache;
+    std::vector<int> devs(ngpus);
+    for (int k = 0; k < ngpus; k++) devs[k] = devices ? devices[k] : k;
+    const std::string hooks = multi_hooks();
+    int rc = RT_OK;
+    if (!(c.m && c.devices == devs && c.w == w && c.h == h)) {
+        destroy_multi(c.m);
+        c.m = nullptr;
+        c.host.clear();
+        if ((rc = spt_multi_create(spheres, nspheres, w, h, devs.data(), ngpus, &c.m))) {
+            c.m = nullptr;
+            return rc;
+        }
+        c.devices = devs;
+        c.w = w;
+        c.h = h;
+        c.host.assign(spheres, spheres + nspheres);
+        c.hooks = hooks;
+        c.contexts++;
+        c.preps++;
+    } else if (!(c.host.size() == nspheres && c.hooks == hooks &&
+                 memcmp(c.host.data(), spheres, sizeof(rt_sphere) * nspheres) == 0)) {
+        c.host.clear();
+        if ((rc = spt_multi_set_scene(c.m, spheres, nspheres))) return rc;
+        c.host.assign(spheres, spheres + nspheres);
+        c.hooks = hooks;
+        c.preps++;
+    }
+    spt_multi *m = c.m;
+    if (counters) {                                    // start from zero (a failed call may have left counts)
+        uint64_t z[4];
+        if ((rc = spt_multi_counters(m, z))) return rc;
+    }
     rc = spt_multi_upload(m, first_sample > 0 ? colors : nullptr, seeds);
     if (rc == RT_OK) rc = spt_multi_render_async(m, camera, first_sample, nsamples, mode, counters != nullptr);
     if (rc == RT_OK) rc = spt_multi_download(m, nsamples > 0 ? colors : nullptr, seeds, nsamples > 0 ? pixels : nullptr);
     if (rc == RT_OK && counters) rc = spt_multi_counters(m, counters);
-    destroy_multi(m);
     return rc;
 }

@@ -22,7 +22,7 @@ EXPORTS = ("rt_last_error", "rt_device_count", "rt_set_device", "rt_release", "r
            "spt_multi_create", "spt_multi_destroy", "spt_multi_set_scene", "spt_multi_bands", "spt_multi_upload",
            "spt_multi_render_async", "spt_multi_gather_async", "spt_multi_sync", "spt_multi_download",
            "spt_multi_read_frame", "spt_multi_counters", "spt_multi_band_buffers", "spt_render_multi",
-           "rtq_render", "rtq_render_async")
+           "spt_multi_cache_info", "rtq_render", "rtq_render_async")
 
 
 class RTError(RuntimeError):
@@ -118,6 +118,8 @@ def lib():
         L.spt_multi_band_buffers.argtypes = [vp, i, ip, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp),
                                              C.POINTER(vp)]
         L.spt_render_multi.argtypes = [vp, u, vp, vp, vp, vp, i, i, i, i, i, u64p, vp, i]
+        if hasattr(L, "spt_multi_cache_info"):
+            L.spt_multi_cache_info.argtypes = [vp]
     if hasattr(L, "rtq_render"):
         L.rtq_render.argtypes = [vp, i, vp, i, i, u64p]
         L.rtq_render_async.argtypes = [vp, i, vp, i, i, i, i, u64p, vp]

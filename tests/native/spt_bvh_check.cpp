@@ -52,10 +52,17 @@ void prepare(Prepared &P, const rt_sphere *sp, int n)
 
 float f32(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 
+float g_K = 2.f;
+int g_mode = 0;          // tools: 1 = re-test a popped child against the current t, 2 = visit order by entry distance
+float g_tn[8];
+int g_first = -1;
+
 // Visit-order hit mask of wide node `nd` (bit p: the child in slot p ^ oct).
-unsigned visit(const Prepared &P, int nd, const float *o, const float *inv, int oct, float alpha, float lim)
+unsigned visit(const Prepared &P, int nd, const float *o, const float *inv, int oct, float alpha, float lim,
+               int idmin = -1)
 {
     const uint32_t *w = &P.wide.words[(size_t)nd * sptbvh::WIDE_WORDS];
+    const uint32_t *hid = &P.wide.maxid[(size_t)nd * sptbvh::WIDE];   // the counted any-hit's pruning
     const float p[3] = {f32(w[0]), f32(w[1]), f32(w[2])};
     const float D0 = f32(w[4]), K = f32(w[5]);
     const float cx = p[0] - o[0], cy = p[1] - o[1], cz = p[2] - o[2];
@@ -73,6 +80,7 @@ unsigned visit(const Prepared &P, int nd, const float *o, const float *inv, int 
     unsigned hm = 0;
     for (int s = 0; s < 8; s++) {
         if (!((w[3] >> (24 + s)) & 1u)) continue;
+        if (idmin >= 0 && (int)hid[s] <= idmin) continue;
         float tn = 0.f, tf = lim;
         for (int k = 0; k < 3; k++) {
             const bool neg = (oct >> k) & 1;
@@ -82,6 +90,7 @@ unsigned visit(const Prepared &P, int nd, const float *o, const float *inv, int 
             tn = std::max(tn, fmaf(qn, a[k], bn[k]));
             tf = std::min(tf, fmaf(qf, a[k], bf[k]));
         }
+        g_tn[s] = tn;
         if (tn <= tf) hm |= 1u << (s ^ oct);
     }
     return hm;
@@ -89,6 +98,8 @@ unsigned visit(const Prepared &P, int nd, const float *o, const float *inv, int 
 
 // The device walk's result for one ray: nearest (t, id) or, shadow, an
 // occluder (the highest index: the counted kernel's IntersectP position).
+long long g_leaves = 0, g_tests = 0;
+
 void walk(const Prepared &P, const float *o, const float *d, bool shadow, float maxt, float &t_out, int &id_out,
           long long &visits)
 {
@@ -107,12 +118,12 @@ void walk(const Prepared &P, const float *o, const float *d, bool shadow, float 
     for (int k = 0; k < 3; k++) dv[k] = fabsf(d[k]) < 1e-30f ? copysignf(1e-30f, d[k]) : d[k];
     const float inv[3] = {1.f / dv[0], 1.f / dv[1], 1.f / dv[2]};
     const float e = fabsf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] - 1.f);
-    const float alpha = e < 0x1p-16f ? 2.f * (1.04e-3f + sqrtf(e + 0x1p-22f)) : 1e30f;
+    const float alpha = e < 0x1p-16f ? g_K * (1.04e-3f + sqrtf(e + 0x1p-22f)) : 1e30f;
     const int oct = (dv[0] < 0.f ? 1 : 0) | (dv[1] < 0.f ? 2 : 0) | (dv[2] < 0.f ? 4 : 0);
     if (P.wide.nnodes > 0) {
         std::vector<uint32_t> stack;
         int cur = 0;
-        unsigned m = visit(P, 0, o, inv, oct, alpha, shadow ? maxt : t);
+        unsigned m = visit(P, 0, o, inv, oct, alpha, shadow ? maxt : t, shadow ? id : -1);
         visits++;
         while (true) {
             while (m == 0 && !stack.empty()) {
@@ -121,12 +132,28 @@ void walk(const Prepared &P, const float *o, const float *d, bool shadow, float 
                 stack.pop_back();
             }
             if (m == 0) break;
-            const int pbit = __builtin_ctz(m);
-            m &= m - 1;
+            int pbit = __builtin_ctz(m);
+            if ((g_mode & 4) && g_first >= 0 && ((m >> g_first) & 1u)) pbit = g_first;
+            g_first = -1;
+            if (g_mode & 2) {                      // nearest entry first (re-tested against the current t)
+                float best = INFINITY;
+                for (unsigned mm = m; mm; mm &= mm - 1) {
+                    const int q = __builtin_ctz(mm);
+                    visit(P, cur, o, inv, oct, alpha, shadow ? maxt : t);
+                    if (g_tn[q ^ oct] < best) { best = g_tn[q ^ oct]; pbit = q; }
+                }
+            }
+            m &= ~(1u << pbit);
             const int s = pbit ^ oct;
+            if (g_mode & 1) {                      // re-test the popped child with the current t
+                const unsigned hm2 = visit(P, cur, o, inv, oct, alpha, shadow ? maxt : t);
+                if (!((hm2 >> pbit) & 1u)) continue;
+            }
             const int32_t cw = (int32_t)P.wide.words[(size_t)cur * sptbvh::WIDE_WORDS + 8 + s];
             if (cw < 0) {
                 const int f = (~cw) & 0xffffff, c = (~cw) >> 24;
+                g_leaves++;
+                g_tests += c;
                 for (int q = 0; q < c; q++) {
                     const int i = P.b2.idx[f + q];
                     const float dd = sphere_hit(P.sp[i], o, d);
@@ -138,10 +165,19 @@ void walk(const Prepared &P, const float *o, const float *d, bool shadow, float 
                     }
                 }
             } else {
-                const unsigned hm = visit(P, cw, o, inv, oct, alpha, shadow ? maxt : t);
+                const unsigned hm = visit(P, cw, o, inv, oct, alpha, shadow ? maxt : t, shadow ? id : -1);
                 visits++;
                 if (hm) {
                     if (m) stack.push_back(((uint32_t)cur << 8) | m);
+                    if (g_mode & 4) {                  // descend into the nearest hit child first
+                        float best = INFINITY;
+                        int bp = -1;
+                        for (unsigned mm = hm; mm; mm &= mm - 1) {
+                            const int q = __builtin_ctz(mm);
+                            if (g_tn[q ^ oct] < best) { best = g_tn[q ^ oct]; bp = q; }
+                        }
+                        g_first = bp;
+                    }
                     if ((int)stack.size() > P.wide.depth - 1) { t_out = NAN; id_out = -2; return; }   // stack bound violated
                     cur = cw;
                     m = hm;
@@ -158,6 +194,16 @@ void walk(const Prepared &P, const float *o, const float *d, bool shadow, float 
 extern "C" {
 
 void spt_bvh_set_leaf_max(int k) { g_leaf_max = k; }
+void spt_bvh_set_mode(int m) { g_mode = m; }
+void spt_bvh_set_k(float k) { g_K = k; }
+
+// Per-ray statistics of the last spt_bvh_wide_check: leaves and spheres tested.
+void spt_bvh_walk_stats(long long *out)
+{
+    out[0] = g_leaves;
+    out[1] = g_tests;
+    g_leaves = g_tests = 0;
+}
 
 // out: binary nodes, wide nodes, wide depth, always spheres, wide bytes
 int spt_bvh_wide_stats(const rt_sphere *sp, int n, long long *out)

@@ -47,6 +47,41 @@ def test_render_multi_repeated_device_bands(rt, nb, w, h):
     assert a.counters == b.counters
 
 
+def _cache_info(rt):
+    import ctypes as C
+    out = (C.c_uint64 * 2)()
+    rt.check(rt.lib().spt_multi_cache_info(out))
+    return out[0], out[1]
+
+
+def test_render_multi_reuses_its_band_context(rt, oracle):
+    """spt_render_multi keeps its band context (scenes, buffers, streams)
+    across calls: a second call with the same devices, size and spheres
+    prepares nothing (contexts and scene preparations unchanged) and is
+    bit-exact; an edited sphere array re-prepares only the scenes; another
+    device list or frame size builds a new context -- every frame exact."""
+    w, h = 160, 120
+    _frame(rt, w, h, 2, devices=[0, 0])              # (context for [0, 0] at 160x120)
+    c0, p0 = _cache_info(rt)
+    a = _frame(rt, w, h, 2, devices=[0, 0])
+    assert _cache_info(rt) == (c0, p0)                # reused: no scene preparation
+    _same(a, _frame(rt, w, h, 2))
+    S, n = rt.scenes.cornell()
+    S[6].p.x += 1.0
+    f = rt.SmallptFrame(w, h, spheres=S, nspheres=n)
+    f.render(2, devices=[0, 0])
+    assert _cache_info(rt) == (c0, p0 + 1)            # scenes re-prepared, same context
+    g = rt.SmallptFrame(w, h, spheres=S, nspheres=n)
+    g.render(2)
+    _same(f, g)
+    b = _frame(rt, w, h, 2, devices=[0, 0, 0])        # another device list: a new context
+    assert _cache_info(rt)[0] == c0 + 1
+    _same(b, _frame(rt, w, h, 2))
+    c = _frame(rt, 96, 64, 3, devices=[0, 0, 0])      # another size: a new context
+    assert _cache_info(rt)[0] == c0 + 2
+    _same(c, _frame(rt, 96, 64, 3))
+
+
 def test_render_multi_direct_lighting(rt):
     a = rt.SmallptFrame(160, 120, mode=rt.SPT_DIRECT_LIGHTING).render(3)
     b = rt.SmallptFrame(160, 120, mode=rt.SPT_DIRECT_LIGHTING).render(3, devices=[0, 0, 0])

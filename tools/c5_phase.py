@@ -37,7 +37,7 @@ def main():
     col = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
     px = torch.zeros(W * H, dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev)
-    nw = ((W + 7) // 8) * ((H + 7) // 8) + 64          # waves of the grid (upper bound)
+    nw = (((W + 7) // 8) * ((H + 7) // 8) + 64) * 8    # work items (upper bound: tiles split up to 8 ways)
     buf = torch.zeros(nw * 16, dtype=torch.int32, device=dev)
 
     K = [0]

@@ -70,16 +70,17 @@ if stats:
     print("  node visits in the first 64 / 256 / 1024 nodes of the ray's octant layout: %.3f %.3f %.3f" % (
         bs[21] / max(bs[0], 1), bs[22] / max(bs[0], 1), bs[23] / max(bs[0], 1)))
 ts = []
+COUNTED = os.environ.get("COUNTED") == "1"          # time the counted kernel instead
 for _ in range(int(os.environ.get("REPS", "1"))):
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(st)
-    run()
+    run(cnt if COUNTED else None)
     b.record(st)
     torch.cuda.synchronize()
     ts.append(a.elapsed_time(b))
 ms = float(np.median(ts))
-print("c5 %dx%d rows [%d,%d) spp=%d spheres=%d: %.2f ms (median of %d, min %.2f), rays %d, %.1f Mrays/s, sphere tests %d" % (
-    W, H, R0, R1, SPP, n, ms, len(ts), min(ts), rays, rays / ms / 1e3, int(cnt[2])))
+print("c5 %dx%d rows [%d,%d) spp=%d spheres=%d%s: %.2f ms (median of %d, min %.2f), rays %d, %.1f Mrays/s, sphere tests %d" % (
+    W, H, R0, R1, SPP, n, " counted" if COUNTED else "", ms, len(ts), min(ts), rays, rays / ms / 1e3, int(cnt[2])))
 if int(cnt[7]):
     q = rays
     print("  per query: %.1f nodes, %.1f sphere tests; lane trips / (64 x wave trips) = %.3f" % (
