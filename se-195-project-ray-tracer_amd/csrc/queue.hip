@@ -865,7 +865,9 @@ int arena(rtrt::DeviceState &st, int w, int rows, rt::queue::QArgs *A)
     const size_t T = (size_t)w * rows * NSUB;
     if (T > (size_t)0x7fffffff / 2) return rtrt::fail(RT_ERR_INVALID, "rtq: frame too large");
     int *ovf = nullptr;
-    size_t P = (size_t)(T * rtrt::pool_fraction(st, rtrt::POOL_QUEUE, (long long)T, POOL_FRAC, &ovf));
+    double frac0 = POOL_FRAC;
+    if (const char *e = getenv("RT_QUEUE_POOL_FRAC0")) frac0 = atof(e);                            // A/B
+    size_t P = (size_t)(T * rtrt::pool_fraction(st, rtrt::POOL_QUEUE, (long long)T, frac0, &ovf));
     if (const char *e = getenv("RT_QUEUE_POOL_CAP")) {      // test hook: exercises the overflow path
         const long long v = atoll(e);
         if (v > 0 && (size_t)v < P) P = (size_t)v;
@@ -955,7 +957,9 @@ extern "C" int rtq_render_async(const rtq_primitive *d_prims, int nprims, uint32
     const float DX = (3.0f - -3.0f) / w, DY = (-2.25f - 2.25f) / h;     // :299-300
     const int rows = row_end - row_begin;
     const int ngroups = (rows + 15) / 16;
-    long long nslab = ((long long)w * ngroups * 16 * rt::queue::NSUB + SLAB_TREES - 1) / SLAB_TREES;
+    long long slab_trees = SLAB_TREES;
+    if (const char *e = getenv("RT_QUEUE_SLAB_TREES")) slab_trees = std::max(100000LL, atoll(e));   // A/B
+    long long nslab = ((long long)w * ngroups * 16 * rt::queue::NSUB + slab_trees - 1) / slab_trees;
     if (const char *e = getenv("RT_QUEUE_SLABS")) nslab = std::max(1, atoi(e));   // test hook
     nslab = std::min<long long>(std::max<long long>(nslab, 1), ngroups);
     const int slab_rows = (int)((ngroups + nslab - 1) / nslab) * 16;

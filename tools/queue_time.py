@@ -29,7 +29,8 @@ def main():
             run()
         e1.record(s)
         torch.cuda.synchronize()
-        print("%dx%d %.4f ms/frame" % (w, h, e0.elapsed_time(e1) / reps), flush=True)
+        print("%dx%d %.4f ms/frame, device arena %.0f MB" % (w, h, e0.elapsed_time(e1) / reps,
+                                                            L.rt_cached_bytes() / 1e6), flush=True)
 
 
 if __name__ == "__main__":
