@@ -3,6 +3,7 @@
 # for each build_ab variant in $LIBS: FETCH_SIZE and WRITE_SIZE passes.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/pmcw
 for v in ${LIBS//,/ }; do
   for c in FETCH_SIZE WRITE_SIZE; do
     RT_HIP_LIB=$GRAFT_REPO_ROOT/build_ab/$v/librt_hip.so SPP=64 REPS=1 timeout -k 10 120 \
