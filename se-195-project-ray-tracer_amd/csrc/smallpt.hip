@@ -918,7 +918,8 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
               int prio_sched, const int *__restrict__ group_order, unsigned *__restrict__ group_cost,
               const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
               const float4 *__restrict__ g_col, const float4 *__restrict__ g_lrec, int nlights,
-              BvhView bvh, unsigned long long *__restrict__ counters, int *__restrict__ work, int split)
+              BvhView bvh, unsigned long long *__restrict__ counters, int *__restrict__ work, int split,
+              int nheavy)
 {
     constexpr bool LDS = GEO == GEO_LDS;
     // GEO_WIDE: persistent waves -- each wave takes 8x8 tiles from a work
@@ -973,21 +974,41 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
 #ifdef RT_SPT_PROF
     unsigned prof_l[PB_N] = {}, prof_w[PB_N] = {};
 #endif
-    // Work item f: tile (f & 3) of dispatch slot f >> 2.  Static launches: one
-    // item per wave, slot (wave >> 2) * gridDim.x + blockIdx.x.  Persistent
-    // launches may split every tile over 2^split items of 64 >> split pixels
-    // (lanes beyond them idle): a tile's pixels then run on several SIMDs.
-    // (split: bits 0..1; the wide walk's options above them, wide_walk)
-    const int nwork = (4 * ((ntiles + 3) >> 2)) << (PERSIST ? (split & 3) : 0);
-    int f = ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) * 4 + (wave & 3);
-    if (PERSIST) {
+    // Work item: tile (item & 3) of dispatch slot item >> 2.  Static launches:
+    // one item per wave, slot (wave >> 2) * gridDim.x + blockIdx.x.
+    // Persistent launches fetch work indices f: the first nheavy items in
+    // dispatch order (the heaviest, with a learnt order) as 2^hs sub-items of
+    // 64 >> hs pixels each (lanes beyond them idle: a heavy tile's pixels run
+    // on several SIMDs), f = (nheavy << hs) + ... the rest whole.
+    // (split: hs in bits 0..1; the wide walk's options above them, wide_walk)
+    const int hs = PERSIST ? (split & 3) : 0;
+    const int nitems = 4 * ((ntiles + 3) >> 2);
+    const int nh = PERSIST ? min(nheavy, nitems) : 0;
+    const int nwork = (nh << hs) + (nitems - nh);
+    // Persistent fetch: waves 0..(4 << hs) - 1 of a block -- 1 << hs per SIMD
+    // -- take the heavy sub-items first (work[1]), the others, and those once
+    // the heavy ones are gone, the rest in order (work[0]): a heavy tile's
+    // SIMD shares its issue slots with lighter, lower-priority waves instead
+    // of with three other heavy tiles.
+    const auto fetch = [&]() {
         int v = 0;
-        if (lane == 0) v = atomicAdd(work, 1);
-        f = __shfl(v, 0, 64);
-    }
+        if (lane == 0) {
+            v = -1;
+            if (wave < (4 << hs) && nh > 0) {
+                const int hv = atomicAdd(work + 1, 1);
+                if (hv < (nh << hs)) v = hv;
+            }
+            if (v < 0) v = (nh << hs) + atomicAdd(work, 1);
+        }
+        return __shfl(v, 0, 64);
+    };
+    int f = ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) * 4 + (wave & 3);
+    if (PERSIST) f = fetch();
     while (!PERSIST || f < nwork) {
-    const int sp_ = PERSIST ? (split & 3) : 0;
-    const int item = f >> sp_, sub = f & ((1 << sp_) - 1);
+    const bool heavy_ = f < (nh << hs);
+    const int sp_ = heavy_ ? hs : 0;
+    const int item = heavy_ ? f >> hs : f - (nh << hs) + nh;
+    const int sub = heavy_ ? f & ((1 << hs) - 1) : 0;
     const int slot = item >> 2;
     const int grp = (SCHED && group_order) ? group_order[slot] : slot;
     const int tile = grp * 4 + (item & 3);
@@ -1533,11 +1554,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     }
 #endif
     if (!PERSIST) break;
-    {
-        int v = 0;
-        if (lane == 0) v = atomicAdd(work, 1);
-        f = __shfl(v, 0, 64);
-    }
+    f = fetch();
     }   // work items
     if (COUNT) {
         const unsigned long long c[4] = {cnt.isect, cnt.isectp, cnt.tests, cnt.samples};
@@ -1618,8 +1635,8 @@ struct spt_scene {
     bool force_global = false;        // RT_SPT_GEO=global: scalar-load path at any size (A/B)
     mutable SptSched sched;           // adaptive group order (hierarchy scenes)
     // Work counters of the persistent (8-wide hierarchy) launches: a ring,
-    // one zeroed counter per launch, so launches in flight on several
-    // streams do not share one.
+    // one zeroed pair (in order, heavy) per launch, so launches in flight on
+    // several streams do not share one.
     static constexpr int NWORK = 64;
     int *d_work = nullptr;
     mutable int work_next = 0;
@@ -1719,20 +1736,26 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     int *work = nullptr;
     if (GEO == rt::smallpt::GEO_WIDE) {
         lds = wide_lds_bytes(sc.bvh.wnodes, sc.bvh.wdepth, g.wpb, COUNT);
-        work = sc.d_work + (sc.work_next++ % spt_scene::NWORK);
-        if (hipMemsetAsync(work, 0, sizeof(int), s) != hipSuccess) return;   // (check_launch reports it)
+        work = sc.d_work + 2 * (sc.work_next++ % spt_scene::NWORK);
+        if (hipMemsetAsync(work, 0, 2 * sizeof(int), s) != hipSuccess) return;   // (check_launch reports it)
+    }
+    int nheavy = 0;                   // with a learnt order: one heavy tile per SIMD of the grid first
+    if (GEO == rt::smallpt::GEO_WIDE && RT_WIDE_PERSIST && g.order) {
+        nheavy = std::min(4 * g.nblocks, 4 * g.nslots);
+        if (const char *e = getenv("RT_WIDE_HEAVY")) nheavy = std::min(std::max(atoi(e), 0), 4 * g.nslots);   // A/B
     }
     int split = 0;
     if (GEO == rt::smallpt::GEO_WIDE) {
         int sp = 0, budget = RT_WIDE_BUDGET, batch = RT_BVH_BATCH, stop = RT_WIDE_STOP;
-        if (const char *e = getenv("RT_SPT_SPLIT")) sp = std::min(std::max(atoi(e), 0), 3);   // tools: tiles split 2^k ways
+        if (const char *e = getenv("RT_SPT_SPLIT")) sp = std::min(std::max(atoi(e), 0), 2);   // A/B: heavy tiles split 2^k ways
         if (const char *e = getenv("RT_WIDE_OPTS")) sscanf(e, "%d,%d,%d", &budget, &batch, &stop);   // tools: A/B
         split = (RT_WIDE_PERSIST ? sp : 0) | (std::min(std::max(budget, 1), 255) << 8) |
                 (std::min(std::max(batch, 0), 64) << 16) | (std::min(std::max(stop, 0), 64) << 24);
     }
     hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.gstride, first,
-                       ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt, work, split);
+                       ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt, work, split,
+                       nheavy);
 }
 
 template <int GEO>
@@ -1812,7 +1835,7 @@ int build_scene_bvh(spt_scene *sc, const rt_sphere *spheres)
     if (e == hipSuccess && wide) e = hipMemcpy(base + w_off, wb.words.data(), w_bytes, hipMemcpyHostToDevice);
     if (e == hipSuccess && wide)
         e = hipMemcpy(base + w_off + w_bytes, wb.maxid.data(), m_bytes, hipMemcpyHostToDevice);
-    if (e == hipSuccess && wide) e = hipMalloc(&sc->d_work, sizeof(int) * spt_scene::NWORK);
+    if (e == hipSuccess && wide) e = hipMalloc(&sc->d_work, 2 * sizeof(int) * spt_scene::NWORK);
     if (e != hipSuccess) return rtrt::fail_hip(e, "spt_scene_create hierarchy upload");
     rt::smallpt::BvhView &v = sc->bvh;
     v.node = (const float4 *)base;

@@ -575,8 +575,11 @@ root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float
 
 // Level L = 1..5: a grid of resident blocks; wave w takes 64-ray pages
 // w, w + #waves, ... of the level's queue.
+#ifndef RT_WH_LEVEL_MINWAVES
+#define RT_WH_LEVEL_MINWAVES RT_WH_MINWAVES
+#endif
 template <bool COUNT>
-__global__ void __launch_bounds__(256, RT_WH_MINWAVES)
+__global__ void __launch_bounds__(256, RT_WH_LEVEL_MINWAVES)
 level_kernel(WfArgs A, int L, unsigned long long *__restrict__ counters)
 {
     __shared__ Scene S;

@@ -272,6 +272,56 @@ def test_adaptive_group_order_is_exact(rt, monkeypatch, sched, walk):
     assert all((k == full[0]).all() for k in full)
 
 
+def test_graph_replay_survives_order_changes(rt):
+    """A launch captured into a graph holds the learnt tile order's device
+    buffer (SptSched): later uncaptured launches of other keys (window, spp)
+    that learn and install new orders -- more tile slots, so a larger buffer
+    -- must neither rewrite nor free it.  Capture a launch of a small window
+    once its order is in use, run two larger keys until theirs are, replay:
+    the bits equal an uncaptured launch of the small window."""
+    import ctypes as C
+    import torch
+    w, h = 480, 270
+    spheres, n, cam = rt.scenes.complex10k()
+    rt.scenes.update_camera(cam, w, h)
+    sc = rt.SmallptScene(spheres, n)
+    dev = torch.device("cuda", 0)
+    seeds0 = torch.from_numpy(rt.scenes.seeds(w, h).view(np.int32)).to(dev)
+
+    def bufs():
+        return (torch.zeros(3 * w * h, dtype=torch.float32, device=dev), torch.zeros_like(seeds0),
+                torch.zeros(w * h, dtype=torch.int32, device=dev))
+
+    def launch(r0, r1, spp, b, stream):
+        col, seeds, px = b
+        rt.check(rt.lib().spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                                 seeds.data_ptr(), px.data_ptr(), w, h, r0, r1, 0, spp, 0, None,
+                                                 stream))
+
+    cur = torch.cuda.current_stream(dev).cuda_stream
+    small = (96, 144, 2)
+    for _ in range(3):                               # record, build the order, use it
+        launch(*small, bufs(), cur)
+    torch.cuda.synchronize()
+    gb = bufs()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="relaxed"):
+        launch(*small, gb, torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    for key in ((0, h, 2), (0, h, 3)):               # new keys, larger order buffers
+        for _ in range(3):
+            launch(*key, bufs(), cur)
+    torch.cuda.synchronize()
+    for t in gb:
+        t.zero_()
+    g.replay()
+    ref = bufs()
+    launch(*small, ref, cur)
+    torch.cuda.synchronize()
+    for a, b in zip(gb, ref):
+        assert (a.cpu().numpy().view(np.uint32) == b.cpu().numpy().view(np.uint32)).all()
+
+
 def _bvh_vs_scan(rt, monkeypatch, spheres, n, cam, w, h, spp, mode=0):
     """Renders with the 8-wide hierarchy, the binary hierarchy (RT_SPT_WIDE=0)
     and the full scan (RT_SPT_NO_BVH), each with and without the work
