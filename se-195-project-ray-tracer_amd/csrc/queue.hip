@@ -467,8 +467,11 @@ struct QArgs {
     float4 *ia;           // queued ray: o.xyz, d.x
     float4 *ib;           // d.y, d.z, weight, tree (bits)
     float4 *ic;           // transparency.xyz, info (bits, pack_info)
+    // A node's record takes its item's place once level_kernel has read it
+    // (no other kernel reads an item after its level): ncol aliases ia, and
+    // nchild[2 q] the first half of ib[q].
     float4 *ncol;         // node term.xyz, counter word (bits)
-    int2 *nchild;         // pool slots of the node's children (levels 1..4)
+    int2 *nchild;         // pool slots of the node's children (levels 1..4), at index 2 q
     int *count;           // [C_TOTAL * CSTRIDE]
     int *ovf;             // host-mapped flag: set when this frame's pool overflowed
     int pool, fixcap, ntrees, npix, w;
@@ -650,7 +653,7 @@ level_kernel(QArgs A, int L)
         }
         if (L < LEVELS - 1) {
             const int2 ch = queue_children(A, S, L, nbase, wave_id, active, f, n, h, tree, node);
-            if (active) A.nchild[q] = ch;
+            if (active) A.nchild[2 * q] = ch;
         }
     }
 }
@@ -690,7 +693,7 @@ __device__ __forceinline__ void fold_tree(const QArgs &A, int tree, int (*ring)[
             for (int i = 0; i < FOLD; i++) {
                 if (q[i] >= 0) {
                     c[i] = A.ncol[q[i]];
-                    cc[i] = inner ? A.nchild[q[i]] : make_int2(-1, -1);
+                    cc[i] = inner ? A.nchild[2 * q[i]] : make_int2(-1, -1);
                 }
             }
 #pragma unroll
@@ -849,7 +852,7 @@ constexpr int SLOT_Q = 8;       // rtrt scratch slot of the queue tracer's arena
 // re-evaluated by final_kernel, exactly, so a denser scene is slower, never
 // wrong (and the next frame's pool is 1.25x larger: rtrt::pool_fraction).
 constexpr long long SLAB_TREES = 12000000;
-constexpr double POOL_FRAC = 0.9;
+constexpr double POOL_FRAC = 0.8;
 
 int wait_frame(rtrt::DeviceState &st)
 {
@@ -878,7 +881,7 @@ int arena(rtrt::DeviceState &st, int w, int rows, rt::queue::QArgs *A)
     const size_t FB = (T + 31) / 32 * 4, PB = (npix + 31) / 32 * 4;
     const size_t FC = std::max<size_t>(npix / 64, 4096);       // listed pixels (fix_kernel)
     const size_t bytes = al(sizeof(Scene)) + al(T * 16) + al(T * 8) + al(npix * 16) + al(FB) + al(PB) +
-                         al(FC * 4) + al(P * 16) * 4 + al(P * 8) + al(sizeof(int) * C_TOTAL * rt::lq::CSTRIDE);
+                         al(FC * 4) + al(P * 16) * 3 + al(sizeof(int) * C_TOTAL * rt::lq::CSTRIDE);
     if (st.cap[SLOT_Q] < bytes && st.wf_pending) {
         int rc = wait_frame(st);
         if (rc) return rc;
@@ -898,8 +901,8 @@ int arena(rtrt::DeviceState &st, int w, int rows, rt::queue::QArgs *A)
     A->ia = (float4 *)take(P * 16);
     A->ib = (float4 *)take(P * 16);
     A->ic = (float4 *)take(P * 16);
-    A->ncol = (float4 *)take(P * 16);
-    A->nchild = (int2 *)take(P * 8);
+    A->ncol = A->ia;
+    A->nchild = (int2 *)A->ib;
     A->count = (int *)take(sizeof(int) * C_TOTAL * rt::lq::CSTRIDE);
     if ((size_t)(p - (char *)base) > bytes) return rtrt::fail(RT_ERR_INVALID, "rtq: arena layout exceeds its size");
     A->ovf = ovf;

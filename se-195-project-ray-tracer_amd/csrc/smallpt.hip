@@ -1809,7 +1809,9 @@ int build_scene_bvh(spt_scene *sc, const rt_sphere *spheres)
     bool wide = false;
     const char *we = getenv("RT_SPT_WIDE");             // 0: the binary walk only (A/B, tests)
     if (nn && !(we && atoi(we) == 0)) {
-        for (int lm : {8, 12, 16}) {
+        int first = 8;                                  // RT_SPT_WIDE_LEAF: A/B of the leaf size
+        if (const char *e = getenv("RT_SPT_WIDE_LEAF")) first = std::min(std::max(atoi(e), 1), 16);
+        for (int lm : {first, 8, 12, 16}) {
             wb.leaf_max = lm;
             wb.build(b);
             if (wide_lds_bytes(wb.nnodes, wb.depth, wide_wpb()) <= WIDE_LDS_MAX) { wide = true; break; }
@@ -2098,15 +2100,16 @@ namespace {
 // synchronises the device to free it on every call.
 struct SceneCache {
     std::vector<rt_sphere> host;
-    std::string hooks;                // the preparation's test hooks (RT_SPT_NO_BVH, RT_SPT_GEO, RT_SPT_WIDE)
+    std::string hooks;                // the preparation's test hooks (RT_SPT_NO_BVH, RT_SPT_GEO, RT_SPT_WIDE[_LEAF])
     spt_scene *sc = nullptr;
 };
 SceneCache g_scene_cache[64];
 
 std::string prep_hooks()
 {
-    const char *a = getenv("RT_SPT_NO_BVH"), *b = getenv("RT_SPT_GEO"), *c = getenv("RT_SPT_WIDE");
-    return std::string(a ? "1" : "0") + "|" + (b ? b : "") + "|" + (c ? c : "");
+    const char *a = getenv("RT_SPT_NO_BVH"), *b = getenv("RT_SPT_GEO"), *c = getenv("RT_SPT_WIDE"),
+               *d = getenv("RT_SPT_WIDE_LEAF");
+    return std::string(a ? "1" : "0") + "|" + (b ? b : "") + "|" + (c ? c : "") + "|" + (d ? d : "");
 }
 
 // Caller holds the device state's lock.

@@ -1,0 +1,13 @@
+set -e
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r03n; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_smallpt.py -x -q --timeout 120 --timeout-method thread > $O/t_smallpt.log 2>&1
+for r in 1 2; do
+for v in pk0 pk1; do
+  for g in "" 3/8 0/8; do
+    echo "lib=$v group=$g" >> $O/pk.log
+    RT_HIP_LIB=$GRAFT_REPO_ROOT/build_ab/$v/librt_hip.so SPP=64 GROUP=$g REPS=5 timeout -k 10 120 python -u tools/c5_time.py >> $O/pk.log 2>&1
+  done
+done
+done
+KERNEL=whitted LIBS=lvl5,lvl6 ROUNDS=3 REPS=5 timeout -k 10 300 python -u tools/ab.py > $O/whitted_lvl.log 2>&1
