@@ -844,7 +844,8 @@ fix_kernel(QArgs A, float DX, float DY, uint32_t *__restrict__ out, unsigned lon
 
 namespace {
 
-constexpr int SLOT_Q = 8;       // rtrt scratch slot of the queue tracer's arena
+constexpr int SLOT_Q = 8;       // rtrt scratch slots of the queue tracer's arenas (two with two streams)
+constexpr int SLOT_Q2 = 10;
 
 // Trees per slab (1080p: two slabs) and the record pool as a fraction of
 // them: the reference scene needs 0.70 (3.02 M nodes below the roots for
@@ -862,7 +863,7 @@ int wait_frame(rtrt::DeviceState &st)
     return RT_OK;
 }
 
-int arena(rtrt::DeviceState &st, int w, int rows, rt::queue::QArgs *A)
+int arena(rtrt::DeviceState &st, int slot, int w, int rows, rt::queue::QArgs *A)
 {
     using namespace rt::queue;
     const size_t T = (size_t)w * rows * NSUB;
@@ -882,12 +883,12 @@ int arena(rtrt::DeviceState &st, int w, int rows, rt::queue::QArgs *A)
     const size_t FC = std::max<size_t>(npix / 64, 4096);       // listed pixels (fix_kernel)
     const size_t bytes = al(sizeof(Scene)) + al(T * 16) + al(T * 8) + al(npix * 16) + al(FB) + al(PB) +
                          al(FC * 4) + al(P * 16) * 3 + al(sizeof(int) * C_TOTAL * rt::lq::CSTRIDE);
-    if (st.cap[SLOT_Q] < bytes && st.wf_pending) {
+    if (st.cap[slot] < bytes && st.wf_pending) {
         int rc = wait_frame(st);
         if (rc) return rc;
     }
     void *base = nullptr;
-    int rc = rtrt::scratch(st, SLOT_Q, bytes, &base);
+    int rc = rtrt::scratch(st, slot, bytes, &base);
     if (rc) return rc;
     char *p = (char *)base;
     auto take = [&](size_t b) { char *q = p; p += al(b); return q; };
@@ -965,32 +966,58 @@ extern "C" int rtq_render_async(const rtq_primitive *d_prims, int nprims, uint32
     long long nslab = ((long long)w * ngroups * 16 * rt::queue::NSUB + slab_trees - 1) / slab_trees;
     if (const char *e = getenv("RT_QUEUE_SLABS")) nslab = std::max(1, atoi(e));   // test hook
     nslab = std::min<long long>(std::max<long long>(nslab, 1), ngroups);
+    // RT_QUEUE_STREAMS=2: slabs alternate between the caller's stream and a
+    // second one, each with its own arena, so one slab's latency-bound fold
+    // runs beside the other's tracing (A/B; at least two slabs then).
+    int nstream = 1;
+    if (const char *e = getenv("RT_QUEUE_STREAMS")) nstream = atoi(e) >= 2 ? 2 : 1;
+    if (nstream == 2) {
+        nslab = std::min<long long>(std::max<long long>(nslab, 2), ngroups);
+        if (nslab < 2) nstream = 1;
+    }
     const int slab_rows = (int)((ngroups + nslab - 1) / nslab) * 16;
-    rt::queue::QArgs A;
-    if ((rc = arena(*st, w, slab_rows, &A))) return rc;
-    A.row_stride = (int)nslab;
+    rt::queue::QArgs A[2];
+    hipStream_t ss[2] = {s, s};
+    if (nstream == 2) {
+        if ((rc = rtrt::aux_stream(*st))) return rc;
+        ss[1] = st->aux;
+        hipError_t e = hipEventRecord(st->fork_ev, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st->aux, st->fork_ev, 0);
+        if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render_async fork");
+    }
     unsigned long long *cnt = (unsigned long long *)d_counters;
-    hipLaunchKernelGGL(rt::queue::scene_kernel, dim3(1), dim3(64), 0, s, d_prims, nprims,
-                       (rt::queue::Scene *)A.scene);
+    for (int i = 0; i < nstream; i++) {
+        if ((rc = arena(*st, i ? SLOT_Q2 : SLOT_Q, w, slab_rows, &A[i]))) return rc;
+        A[i].row_stride = (int)nslab;
+        hipLaunchKernelGGL(rt::queue::scene_kernel, dim3(1), dim3(64), 0, ss[i], d_prims, nprims,
+                           (rt::queue::Scene *)A[i].scene);
+    }
+    // RT_QUEUE_EXACT_ALL=1 (test hook): every specular term uncertified,
+    // so fix_kernel's exact path renders nearly every pixel.
+    const char *ex = getenv("RT_QUEUE_EXACT_ALL");
     for (int k = 0; k < (int)nslab; k++) {
+        rt::queue::QArgs &a = A[k % nstream];
+        hipStream_t sk = ss[k % nstream];
         const int srows = (int)((ngroups - k + nslab - 1) / nslab) * 16;
-        A.row_begin = row_begin + 16 * k;
-        A.npix = w * srows;
-        A.ntrees = A.npix * rt::queue::NSUB;
-        hipError_t e = hipMemsetAsync(A.count, 0, sizeof(int) * rt::queue::C_TOTAL * rt::lq::CSTRIDE, s);
-        if (e == hipSuccess) e = hipMemsetAsync(A.fixbits, 0, sizeof(unsigned) * (((size_t)A.ntrees + 31) / 32), s);
-        if (e == hipSuccess) e = hipMemsetAsync(A.pixbits, 0, sizeof(unsigned) * (((size_t)A.npix + 31) / 32), s);
+        a.row_begin = row_begin + 16 * k;
+        a.npix = w * srows;
+        a.ntrees = a.npix * rt::queue::NSUB;
+        hipError_t e = hipMemsetAsync(a.count, 0, sizeof(int) * rt::queue::C_TOTAL * rt::lq::CSTRIDE, sk);
+        if (e == hipSuccess) e = hipMemsetAsync(a.fixbits, 0, sizeof(unsigned) * (((size_t)a.ntrees + 31) / 32), sk);
+        if (e == hipSuccess) e = hipMemsetAsync(a.pixbits, 0, sizeof(unsigned) * (((size_t)a.npix + 31) / 32), sk);
         if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render_async memset");
-        // RT_QUEUE_EXACT_ALL=1 (test hook): every specular term uncertified,
-        // so fix_kernel's exact path renders nearly every pixel.
-        const char *ex = getenv("RT_QUEUE_EXACT_ALL");
         if (ex && *ex == '1')
-            rc = cnt ? launch<true, true>(A, w, srows, row_end, DX, DY, cnt, s, d_pixels)
-                     : launch<false, true>(A, w, srows, row_end, DX, DY, cnt, s, d_pixels);
+            rc = cnt ? launch<true, true>(a, w, srows, row_end, DX, DY, cnt, sk, d_pixels)
+                     : launch<false, true>(a, w, srows, row_end, DX, DY, cnt, sk, d_pixels);
         else
-            rc = cnt ? launch<true, false>(A, w, srows, row_end, DX, DY, cnt, s, d_pixels)
-                     : launch<false, false>(A, w, srows, row_end, DX, DY, cnt, s, d_pixels);
+            rc = cnt ? launch<true, false>(a, w, srows, row_end, DX, DY, cnt, sk, d_pixels)
+                     : launch<false, false>(a, w, srows, row_end, DX, DY, cnt, sk, d_pixels);
         if (rc) return rc;
+    }
+    if (nstream == 2) {
+        hipError_t e = hipEventRecord(st->join_ev, st->aux);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, st->join_ev, 0);
+        if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render_async join");
     }
     hipError_t e = hipEventRecord(st->wf_done, s);
     if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render_async record");

@@ -26,11 +26,31 @@ void release_state(DeviceState *st)
     for (int i = 0; i < NSCRATCH; i++)
         if (st->buf[i]) (void)hipFree(st->buf[i]);
     if (st->pool_ovf) (void)hipHostFree(st->pool_ovf);   // host-mapped overflow flags
+    if (st->aux) (void)hipStreamSynchronize(st->aux);
     if (st->wf_done) (void)hipEventDestroy(st->wf_done);
+    if (st->fork_ev) (void)hipEventDestroy(st->fork_ev);
+    if (st->join_ev) (void)hipEventDestroy(st->join_ev);
+    if (st->aux) (void)hipStreamDestroy(st->aux);
     if (st->stream) (void)hipStreamDestroy(st->stream);
     delete st;
 }
 }  // namespace
+
+int aux_stream(DeviceState &st)
+{
+    if (st.aux) return RT_OK;
+    hipError_t e = hipEventCreateWithFlags(&st.fork_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&st.join_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&st.aux, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        if (st.fork_ev) (void)hipEventDestroy(st.fork_ev);
+        if (st.join_ev) (void)hipEventDestroy(st.join_ev);
+        st.fork_ev = st.join_ev = nullptr;
+        st.aux = nullptr;
+        return fail_hip(e, "aux stream");
+    }
+    return RT_OK;
+}
 
 int fail(int code, const char *msg)
 {

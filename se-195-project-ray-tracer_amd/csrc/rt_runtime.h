@@ -11,7 +11,7 @@
 
 namespace rtrt {
 
-constexpr int NSCRATCH = 9;
+constexpr int NSCRATCH = 11;
 constexpr int SLOT_VIEW = 7;
 
 struct DeviceState {
@@ -46,6 +46,10 @@ struct DeviceState {
     int pool_fit_next = 0;
     int *pool_ovf = nullptr;           // host-mapped [16]
     int *pool_ovf_dev = nullptr;       // its device address
+    // A second stream for the level pass's concurrent slabs (aux_stream):
+    // forked from and joined back to the caller's stream by events.
+    hipStream_t aux = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
 };
 
 constexpr int POOL_WHITTED = 0, POOL_QUEUE = 1, POOL_FITS = 16;
@@ -64,6 +68,8 @@ int scratch(DeviceState &st, int slot, size_t bytes, void **out);
 // per slab (starts at `initial`; grown after an overflowed frame of that
 // size) and, in *flag_dev, the device address of that entry's overflow flag.
 double pool_fraction(DeviceState &st, int which, long long trees, double initial, int **flag_dev);
+// The state's second stream and its fork / join events (created on first use).
+int aux_stream(DeviceState &st);
 // Frees the per-device scenes cached by spt_render / spt_render_async
 // (smallpt.hip; rt_release).
 void release_cached_scenes();

@@ -920,7 +920,8 @@ fixup_kernel(WfArgs A, const float *__restrict__ sx_tab, const float *__restrict
 
 namespace {
 
-constexpr int SLOT_WF = 6;      // rtrt scratch slot of the level-pass arena
+constexpr int SLOT_WF = 6;      // rtrt scratch slots of the level-pass arenas (two with two streams)
+constexpr int SLOT_WF2 = 9;
 
 // Trees per slab of the level pass.  A frame with more trees is rendered as
 // several slabs, one after the other on the stream, so the arena is sized
@@ -928,6 +929,7 @@ constexpr int SLOT_WF = 6;      // rtrt scratch slot of the level-pass arena
 // interleave in groups of 16 rows (slab_row), so every slab holds the
 // frame's mix of sphere / plane / background rows and so its queue fill.
 constexpr long long SLAB_TREES = 18000000;
+constexpr long long STREAM2_TREES = 4000000;   // frames from this size on: two slabs on two streams
 // Record pool (levels 1..5 together) as a fraction of the slab's trees, to
 // start with.  The reference scene needs 0.83 at 1080p (14.2 M nodes for
 // 17.1 M trees) but 0.94 at 640 x 480 (its rows [20, 410) hold more of the
@@ -1001,7 +1003,7 @@ int view_tables(rtrt::DeviceState &st, hipStream_t s, int w, int h, bool ocl, fl
 // Device arena of the level pass (scratch slot SLOT_WF, grow-only) for a slab
 // of `rows` rows: per tree a root record and a fixup bit; the record pool of
 // levels 1..5; per level 0..4 a TIR list.
-int wavefront_arena(rtrt::DeviceState &st, int w, int rows, int nsub, rt::whitted::WfArgs *A)
+int wavefront_arena(rtrt::DeviceState &st, int slot, int w, int rows, int nsub, rt::whitted::WfArgs *A)
 {
     using namespace rt::whitted;
     const size_t T = (size_t)w * rows * nsub;
@@ -1024,7 +1026,7 @@ int wavefront_arena(rtrt::DeviceState &st, int w, int rows, int nsub, rt::whitte
     const size_t bytes = al(sizeof(Scene)) + root_b + pool_b + (LEVELS - 1) * al(TC * 16) +
                          al(sizeof(int) * C_TOTAL * CSTRIDE);
     void *base = nullptr;
-    int rc = frame_scratch(st, SLOT_WF, bytes, &base);
+    int rc = frame_scratch(st, slot, bytes, &base);
     if (rc) return rc;
     char *p = (char *)base;
     auto take = [&](size_t b) { char *q = p; p += al(b); return q; };
@@ -1106,26 +1108,56 @@ int render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int 
     long long nslab = ((long long)w * ngroups * 16 * nsub + SLAB_TREES - 1) / SLAB_TREES;
     if (const char *e = getenv("RT_WHITTED_SLABS")) nslab = std::max(1, atoi(e));   // test hook
     nslab = std::min<long long>(std::max<long long>(nslab, 1), ngroups);
+    // Frames of >= 4 M trees run as (at least) two slabs that alternate
+    // between the caller's stream and a second one, each with its own arena:
+    // one slab's launches fill the tails of the other's, and its
+    // HBM-bound back-accumulation runs beside the other's tracing (1080p:
+    // 2.00 -> 1.85 ms; the same two slabs on one stream: 2.15 ms).
+    // RT_WHITTED_STREAMS=1/2 overrides (A/B).
+    int nstream = (long long)w * ngroups * 16 * nsub >= STREAM2_TREES ? 2 : 1;
+    if (const char *e = getenv("RT_WHITTED_STREAMS")) nstream = atoi(e) >= 2 ? 2 : 1;
+    if (nstream == 2) {
+        nslab = std::min<long long>(std::max<long long>(nslab, 2), ngroups);
+        if (nslab < 2) nstream = 1;
+    }
     const int slab_rows = (int)((ngroups + nslab - 1) / nslab) * 16;
-    rt::whitted::WfArgs A;
-    if ((rc = wavefront_arena(*st, w, slab_rows, nsub, &A))) return rc;
-    A.side = side;
-    A.nsub = nsub;
-    A.ocl = ocl;
-    A.row_stride = (int)nslab;
+    rt::whitted::WfArgs A[2];
+    hipStream_t ss[2] = {s, s};
+    if (nstream == 2) {
+        if ((rc = rtrt::aux_stream(*st))) return rc;
+        ss[1] = st->aux;
+        hipError_t e = hipEventRecord(st->fork_ev, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st->aux, st->fork_ev, 0);
+        if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async fork");
+    }
     unsigned long long *cnt = (unsigned long long *)d_counters;
-    hipLaunchKernelGGL(rt::whitted::scene_kernel, dim3(1), dim3(64), 0, s, d_prims, nprims, (rt::whitted::Scene *)A.scene);
+    for (int i = 0; i < nstream; i++) {
+        if ((rc = wavefront_arena(*st, i ? SLOT_WF2 : SLOT_WF, w, slab_rows, nsub, &A[i]))) return rc;
+        A[i].side = side;
+        A[i].nsub = nsub;
+        A[i].ocl = ocl;
+        A[i].row_stride = (int)nslab;
+        hipLaunchKernelGGL(rt::whitted::scene_kernel, dim3(1), dim3(64), 0, ss[i], d_prims, nprims,
+                           (rt::whitted::Scene *)A[i].scene);
+    }
     for (int k = 0; k < (int)nslab; k++) {
+        rt::whitted::WfArgs &a = A[k % nstream];
+        hipStream_t sk = ss[k % nstream];
         const int srows = (int)((ngroups - k + nslab - 1) / nslab) * 16;
-        A.row_begin = row_begin + 16 * k;
-        A.npix = w * srows;
-        A.ntrees = A.npix * nsub;
-        hipError_t e = hipMemsetAsync(A.count, 0, sizeof(int) * rt::whitted::C_TOTAL * rt::whitted::CSTRIDE, s);
-        if (e == hipSuccess) e = hipMemsetAsync(A.fixbits, 0, sizeof(unsigned) * (((size_t)A.ntrees + 31) / 32), s);
+        a.row_begin = row_begin + 16 * k;
+        a.npix = w * srows;
+        a.ntrees = a.npix * nsub;
+        hipError_t e = hipMemsetAsync(a.count, 0, sizeof(int) * rt::whitted::C_TOTAL * rt::whitted::CSTRIDE, sk);
+        if (e == hipSuccess) e = hipMemsetAsync(a.fixbits, 0, sizeof(unsigned) * (((size_t)a.ntrees + 31) / 32), sk);
         if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async memset");
-        rc = cnt ? launch_wavefront<true>(A, w, srows, row_end, d_sx, d_sy, DX, DY, cnt, s, d_xrgb)
-                 : launch_wavefront<false>(A, w, srows, row_end, d_sx, d_sy, DX, DY, cnt, s, d_xrgb);
+        rc = cnt ? launch_wavefront<true>(a, w, srows, row_end, d_sx, d_sy, DX, DY, cnt, sk, d_xrgb)
+                 : launch_wavefront<false>(a, w, srows, row_end, d_sx, d_sy, DX, DY, cnt, sk, d_xrgb);
         if (rc) return rc;
+    }
+    if (nstream == 2) {
+        hipError_t e = hipEventRecord(st->join_ev, st->aux);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, st->join_ev, 0);
+        if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async join");
     }
     hipError_t e = hipEventRecord(st->wf_done, s);
     if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async record");
