@@ -847,12 +847,12 @@ namespace {
 constexpr int SLOT_Q = 8;       // rtrt scratch slots of the queue tracer's arenas (two with two streams)
 constexpr int SLOT_Q2 = 10;
 
-// Trees per slab (1080p: two slabs) and the record pool as a fraction of
+// Trees per slab (1080p: three slabs, on two streams) and the record pool as a fraction of
 // them: the reference scene needs 0.70 (3.02 M nodes below the roots for
 // 4.32 M trees at 800 x 600); a tree with a node that does not fit is
 // re-evaluated by final_kernel, exactly, so a denser scene is slower, never
 // wrong (and the next frame's pool is 1.25x larger: rtrt::pool_fraction).
-constexpr long long SLAB_TREES = 12000000;
+constexpr long long SLAB_TREES = 6000000;
 constexpr double POOL_FRAC = 0.8;
 
 int wait_frame(rtrt::DeviceState &st)
@@ -966,10 +966,13 @@ extern "C" int rtq_render_async(const rtq_primitive *d_prims, int nprims, uint32
     long long nslab = ((long long)w * ngroups * 16 * rt::queue::NSUB + slab_trees - 1) / slab_trees;
     if (const char *e = getenv("RT_QUEUE_SLABS")) nslab = std::max(1, atoi(e));   // test hook
     nslab = std::min<long long>(std::max<long long>(nslab, 1), ngroups);
-    // RT_QUEUE_STREAMS=2: slabs alternate between the caller's stream and a
-    // second one, each with its own arena, so one slab's latency-bound fold
-    // runs beside the other's tracing (A/B; at least two slabs then).
-    int nstream = 1;
+    // A frame of several slabs alternates them between the caller's stream
+    // and a second one, each with its own arena: one slab's latency-bound
+    // fold runs beside the other's tracing (1080p, three 6 M-tree slabs:
+    // 1.80 -> 1.57 ms at the same 605 MB of arenas; one slab per stream at
+    // 12 M: 1.50 ms but 1.2 GB). RT_QUEUE_STREAMS=1/2 overrides (A/B; 2
+    // forces at least two slabs).
+    int nstream = nslab >= 2 ? 2 : 1;
     if (const char *e = getenv("RT_QUEUE_STREAMS")) nstream = atoi(e) >= 2 ? 2 : 1;
     if (nstream == 2) {
         nslab = std::min<long long>(std::max<long long>(nslab, 2), ngroups);
