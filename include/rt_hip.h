@@ -103,7 +103,10 @@ int rtw_render(const rt_primitive *prims, int nprims, uint32_t *xrgb, int w, int
 
 /* Asynchronous, device-resident.  d_prims: device copy of the primitive
  * array; d_xrgb: device frame (w*h); d_counters: device u64[4] accumulated
- * into (nullable); stream: hipStream_t (NULL = default stream). */
+ * into (nullable); stream: hipStream_t (NULL = default stream).  Work is
+ * ordered on `stream`: a large frame also runs on a library-owned second
+ * stream, forked from `stream` and joined back to it by events before the
+ * call's last operation. */
 int rtw_render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int w, int h,
                      int row_begin, int row_end, uint64_t *d_counters, void *stream);
 
@@ -271,7 +274,9 @@ int rtq_render(const rtq_primitive *prims, int nprims, uint32_t *pixels, int w, 
                uint64_t *counters);
 /* Asynchronous, device-resident: rows [row_begin,row_end) of the w x h frame
  * (0 <= row_begin < row_end <= h; other rows untouched) into d_pixels (w*h);
- * d_counters: device u64[4] accumulated into (nullable). */
+ * d_counters: device u64[4] accumulated into (nullable).  Ordered on
+ * `stream` as rtw_render_async (a frame of several slabs also uses the
+ * library's second stream, forked and joined by events). */
 int rtq_render_async(const rtq_primitive *d_prims, int nprims, uint32_t *d_pixels, int w, int h,
                      int row_begin, int row_end, uint64_t *d_counters, void *stream);
 
