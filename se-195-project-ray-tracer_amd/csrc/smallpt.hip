@@ -825,6 +825,225 @@ __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigne
     return done;
 }
 
+// ---------------------------------------------------------------------------
+// Cooperative 8-wide walk: EIGHT lanes per ray (the heaviest tiles).
+//
+// A heavy tile's critical path is one pixel's 64-sample RNG chain of ~900
+// loop iterations, each ~24 dependent walk trips; a lone wave issues one VALU
+// instruction per ~4 cycles, and a per-lane trip (eight child slab tests, the
+// stack, the pending-leaf bookkeeping) costs it ~250 of them.  Here the eight
+// lanes of a lane group (lanes 8g .. 8g+7) hold the same pixel -- the same
+// ray, RNG words and path state, computed redundantly and identically -- and
+// split each trip: lane k tests child slot k ^ oct of the node (its bit of the
+// visit mask, gathered with one ballot), or sphere k of a leaf (the group's
+// nearest / any hit by a 3-step DPP reduction).  A trip is ~40 VALU
+// instructions instead of ~250, a leaf is one pass instead of up to four, and
+// the wave walks the maximum over 8 rays instead of 64.  Group-uniform state
+// (node, mask, stack, t, bpos, id) is held identically by the 8 lanes; each
+// lane keeps its own copy of the stack column, as in wide_walk.  Results are
+// the reference's: every sphere a per-lane walk would test is tested with
+// the same float formula, and the nearest hit is the minimum distance with
+// the highest reference index on ties, an order-independent choice.
+__device__ __forceinline__ int dpp_xor1(int v) { return __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ int dpp_xor2(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false); }
+__device__ __forceinline__ int dpp_mir8(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false); }
+__device__ __forceinline__ float grp8_min(float v)
+{
+    v = fminf(v, __int_as_float(dpp_xor1(__float_as_int(v))));
+    v = fminf(v, __int_as_float(dpp_xor2(__float_as_int(v))));
+    return fminf(v, __int_as_float(dpp_mir8(__float_as_int(v))));
+}
+__device__ __forceinline__ int grp8_max(int v)
+{
+    v = max(v, dpp_xor1(v));
+    v = max(v, dpp_xor2(v));
+    return max(v, dpp_mir8(v));
+}
+// The group's 8 bits of a predicate (bit k = lane 8g + k).
+__device__ __forceinline__ unsigned grp8_bits(bool p, int gbase)
+{
+    return (unsigned)(__builtin_amdgcn_ballot_w64(p) >> gbase) & 255u;
+}
+
+// wide_visit for one child slot per lane: lane k of the group tests slot
+// k ^ oct and the group's visit mask (bit k) comes back from a ballot.  The
+// float operations are wide_visit's, so the culling decisions are its own.
+__device__ __forceinline__ unsigned wide_visit_coop(const uint4 *__restrict__ N, const ray3 &r, float ix, float iy,
+                                                    float iz, float alpha, int oct, float lim, int pos, int gbase,
+                                                    const unsigned *__restrict__ hid = nullptr, int idmin = -1)
+{
+    const uint4 h0 = N[0];
+    const float2 h1 = *(const float2 *)(N + 1);
+    const int sl = pos ^ oct;
+    const unsigned *q = (const unsigned *)N + 16 + 6 * (sl >> 2);
+    const uint2 w0 = *(const uint2 *)q, w1 = *(const uint2 *)(q + 2), w2 = *(const uint2 *)(q + 4);
+    const float cx = __uint_as_float(h0.x) - r.o.x, cy = __uint_as_float(h0.y) - r.o.y,
+                cz = __uint_as_float(h0.z) - r.o.z;
+    const float dist = __builtin_amdgcn_sqrtf(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, cz * cz)));
+    const float m = __builtin_fmaf(alpha, dist + h1.x, h1.y);
+    const float ax = __uint_as_float((h0.w & 255u) << 23) * ix;
+    const float ay = __uint_as_float(((h0.w >> 8) & 255u) << 23) * iy;
+    const float az = __uint_as_float(((h0.w >> 16) & 255u) << 23) * iz;
+    const float bx = cx * ix, by = cy * iy, bz = cz * iz;
+    const float mx = m * fabsf(ix), my = m * fabsf(iy), mz = m * fabsf(iz);
+    const float bnx = bx - mx, bfx = bx + mx, bny = by - my, bfy = by + my, bnz = bz - mz, bfz = bz + mz;
+    const unsigned lx = w0.x, ly = w0.y, lz = w1.x, ux = w1.y, uy = w2.x, uz = w2.y;
+    const unsigned nxw = (oct & 1) ? ux : lx, fxw = (oct & 1) ? lx : ux;
+    const unsigned nyw = (oct & 2) ? uy : ly, fyw = (oct & 2) ? ly : uy;
+    const unsigned nzw = (oct & 4) ? uz : lz, fzw = (oct & 4) ? lz : uz;
+    const int sh = 8 * (sl & 3);
+    const float tnx = __builtin_fmaf((float)((nxw >> sh) & 255u), ax, bnx);
+    const float tfx = __builtin_fmaf((float)((fxw >> sh) & 255u), ax, bfx);
+    const float tny = __builtin_fmaf((float)((nyw >> sh) & 255u), ay, bny);
+    const float tfy = __builtin_fmaf((float)((fyw >> sh) & 255u), ay, bfy);
+    const float tnz = __builtin_fmaf((float)((nzw >> sh) & 255u), az, bnz);
+    const float tfz = __builtin_fmaf((float)((fzw >> sh) & 255u), az, bfz);
+    const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.f));
+    const float tf = fminf(fminf(tfx, tfy), fminf(tfz, lim));
+    bool hit = tn <= tf && ((h0.w >> (24 + sl)) & 1u);
+    if (hid && idmin >= 0) hit = hit && (int)hid[sl] > idmin;
+    return grp8_bits(hit, gbase);
+}
+
+// One leaf (first sphere f, c spheres) for the group: sphere b + k on lane k.
+// Nearest hit: t / bpos updated to the minimum distance, highest reference
+// index on ties (ids loaded only then).  Any hit: COUNT -- id = the highest
+// occluder index so far; otherwise bpos = f marks "occluded" and the caller
+// ends the walk.
+template <bool COUNT>
+__device__ __forceinline__ void leaf_coop(const BvhView &B, const ray3 &r, bool shadow, float maxt, int f, int c,
+                                          int pos, int gbase, float &t, int &bpos, int &id)
+{
+    for (int b = 0; b < c; b += 8) {
+        const int q = b + pos;
+        const bool have = q < c;
+        const float4 g = B.geo[f + (have ? q : 0)];
+        const float opx = g.x - r.o.x, opy = g.y - r.o.y, opz = g.z - r.o.z;
+        const float bb = opx * r.d.x + opy * r.d.y + opz * r.d.z;
+        const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g.w;
+        float d;
+        if (wave_any(have && fabsf(det) < 0x1p-96f)) {
+            d = sphere_hit(g, r);
+        } else {
+            const float sd = sqrt_nr(det);
+            const float t1 = bb - sd, t2 = bb + sd;
+            d = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
+        }
+        if (!have) d = MISS;
+        if (shadow) {
+            const bool occ = d < maxt;
+            if (COUNT) {
+                int i = -1;
+                if (grp8_bits(occ, gbase)) {
+                    if (occ) i = B.id[f + q];
+                    i = grp8_max(i);
+                }
+                if (i > id) id = i;
+            } else if (grp8_bits(occ, gbase)) {
+                bpos = f;
+                return;
+            }
+        } else {
+            const float dm = grp8_min(d);
+            if (dm <= t) {                      // (dm finite: t < +inf)
+                const unsigned cm = grp8_bits(d == dm, gbase);
+                if (dm < t && __builtin_popcount(cm) == 1) {
+                    t = dm;
+                    bpos = f + b + __builtin_ctz(cm);
+                } else {                        // a tie: within the leaf, or with the best so far
+                    int i = -1;
+                    if (d == dm) i = B.id[f + q];
+                    const int im = grp8_max(i);
+                    const int cur_id = dm == t ? (bpos >= 0 ? B.id[bpos] : id) : -1;
+                    if (im > cur_id) {
+                        t = dm;
+                        bpos = f + b + __builtin_ctz(grp8_bits(i == im, gbase));
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <bool COUNT>
+__device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, unsigned *__restrict__ stk,
+                               const ray3 &r, bool shadow, BvhWalk &W, int opts)
+{
+    const int budget = (opts >> 8) & 255, stop = (opts >> 24) & 255;
+    const float maxt = W.t;
+    float t = W.t;
+    int id = W.id, cur = W.node, sp = W.sp, bpos = W.bpos;
+    unsigned m = W.m;
+    const float dx = fabsf(r.d.x) < 1e-30f ? copysignf(1e-30f, r.d.x) : r.d.x;
+    const float dy = fabsf(r.d.y) < 1e-30f ? copysignf(1e-30f, r.d.y) : r.d.y;
+    const float dz = fabsf(r.d.z) < 1e-30f ? copysignf(1e-30f, r.d.z) : r.d.z;
+    const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
+    const float e = fabsf(r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z - 1.f);
+    const float alpha = e < 0x1p-16f ? BVH_K * (1.04e-3f + __builtin_amdgcn_sqrtf(e + 0x1p-22f)) : 1e30f;
+    const int oct = (dx < 0.f ? 1 : 0) | (dy < 0.f ? 2 : 0) | (dz < 0.f ? 4 : 0);
+    const unsigned *Lw = (const unsigned *)L;
+    const unsigned *Lmax = COUNT ? (const unsigned *)(L + 7 * B.wnodes) : nullptr;
+    unsigned *my = stk + (threadIdx.x & 63);
+    const int pos = threadIdx.x & 7, gbase = threadIdx.x & 56;
+    const int n0 = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true));
+    int trips = 0;
+    while (true) {
+        if (m != 0) {
+            int cw;
+            if (cur < 0) {
+                cw = 0;
+                m = 0;
+            } else {
+                const int p = __builtin_ctz(m);
+                m &= m - 1;
+                cw = (int)Lw[cur * WIDE_WORDS + 8 + (p ^ oct)];
+            }
+            if (cw < 0) {
+                const int lf = ~cw;
+                leaf_coop<COUNT>(B, r, shadow, maxt, lf & 0xffffff, lf >> 24, pos, gbase, t, bpos, id);
+                if (!COUNT && shadow && bpos >= 0) {
+                    m = 0;
+                    sp = 0;
+                }
+            } else {
+                const unsigned hm =
+                    COUNT ? wide_visit_coop(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase,
+                                            Lmax + 8 * cw, shadow ? id : -1)
+                          : wide_visit_coop(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase);
+                if (hm) {
+                    if (m) {
+                        my[64 * sp] = ((unsigned)cur << 8) | m;
+                        sp++;
+                    }
+                    cur = cw;
+                    m = hm;
+                }
+            }
+            if (m == 0 && sp > 0) {
+                sp--;
+                const unsigned e2 = my[64 * sp];
+                cur = (int)(e2 >> 8);
+                m = e2 & 255u;
+            }
+        }
+        trips++;
+        const unsigned long long am = __builtin_amdgcn_ballot_w64(m != 0);
+        if (am == 0 || trips >= budget || 64 * __builtin_popcountll(am) <= stop * n0) break;
+    }
+#ifdef RT_SPT_TRACE
+    W.tr_trips += trips;
+#endif
+    const bool done = m == 0;
+    if (done && bpos >= 0) id = (!COUNT && shadow) ? 0x7fffffff : B.id[bpos];
+    W.t = t;
+    W.id = id;
+    W.bpos = bpos;
+    W.node = cur;
+    W.m = m;
+    W.sp = sp;
+    return done;
+}
+
 struct Counts { unsigned long long isect, isectp, tests, samples; };
 
 // Tools-only block profile (build with -DRT_SPT_PROF; tools/ab.py PROF=1):
@@ -1003,16 +1222,23 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         return __shfl(v, 0, 64);
     };
     int f = ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) * 4 + (wave & 3);
-    if (PERSIST) f = fetch();
+    if (PERSIST) f = __builtin_amdgcn_readfirstlane(fetch());
     while (!PERSIST || f < nwork) {
     const bool heavy_ = f < (nh << hs);
-    const int sp_ = heavy_ ? hs : 0;
+    // hs = 3 (COOP): a heavy tile's 8 sub-items are 8 rows of 8 pixels with
+    // eight lanes per pixel (lane group g = pixel g of the row), walking the
+    // hierarchy cooperatively (wide_walk_coop).  Otherwise a sub-item is
+    // 64 >> hs pixels, a lane each.
+    const bool coop = GEO == GEO_WIDE && heavy_ && hs == 3;
+    const int sp_ = heavy_ && !coop ? hs : 0;
     const int item = heavy_ ? f >> hs : f - (nh << hs) + nh;
     const int sub = heavy_ ? f & ((1 << hs) - 1) : 0;
     const int slot = item >> 2;
     const int grp = (SCHED && group_order) ? group_order[slot] : slot;
     const int tile = grp * 4 + (item & 3);
-    const int li = (sub << (6 - sp_)) + lane;           // pixel of the 8x8 tile (valid: lane < 64 >> split)
+    const int li = coop ? (sub << 3) + (lane >> 3)      // pixel of the 8x8 tile (valid: lane < 64 >> split)
+                        : (sub << (6 - sp_)) + lane;
+    const bool lead = !coop || (lane & 7) == 0;         // the lane that stores the pixel and counts
     unsigned long long t_start = 0;
     if (SCHED) t_start = __builtin_amdgcn_s_memrealtime();
     // GSTORE (hierarchy kernels): per group of the block a 32x8 staging
@@ -1218,7 +1444,8 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 tr_queries += !walking;
 #endif
                 if (!walking) wide_begin<COUNT>(bvh, ray, shadow, t, walk);
-                walking = !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
+                walking = coop ? !wide_walk_coop<COUNT>(bvh, wL, wstk, ray, shadow, walk, split)
+                               : !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
 #ifdef RT_SPT_TRACE
                 tr_walk += (unsigned)(__builtin_amdgcn_s_memtime() - tr_w0);
 #endif
@@ -1465,7 +1692,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             }
             gs_seed[r * 64 + 2 * c] = s0;
             gs_seed[r * 64 + 2 * c + 1] = s1;
-        } else {
+        } else if (lead) {
             if (nsamples > 0) {
                 colors[3 * (size_t)i] = col.x;
                 colors[3 * (size_t)i + 1] = col.y;
@@ -1553,8 +1780,14 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         }
     }
 #endif
+    if (COUNT && PERSIST && hs == 3) {                  // a cooperative group counts its pixel once:
+        if (!lead) cnt = Counts{0, 0, 0, 0};            //   flushed per work item
+        const unsigned long long c[4] = {cnt.isect, cnt.isectp, cnt.tests, cnt.samples};
+        flush_counters<4>(counters, c);
+        cnt = Counts{0, 0, 0, 0};
+    }
     if (!PERSIST) break;
-    f = fetch();
+    f = __builtin_amdgcn_readfirstlane(fetch());
     }   // work items
     if (COUNT) {
         const unsigned long long c[4] = {cnt.isect, cnt.isectp, cnt.tests, cnt.samples};
@@ -1747,7 +1980,8 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     int split = 0;
     if (GEO == rt::smallpt::GEO_WIDE) {
         int sp = 0, budget = RT_WIDE_BUDGET, batch = RT_BVH_BATCH, stop = RT_WIDE_STOP;
-        if (const char *e = getenv("RT_SPT_SPLIT")) sp = std::min(std::max(atoi(e), 0), 2);   // A/B: heavy tiles split 2^k ways
+        // heavy tiles split 2^k ways (A/B), k = 3: 8 lanes per pixel (wide_walk_coop)
+        if (const char *e = getenv("RT_SPT_SPLIT")) sp = std::min(std::max(atoi(e), 0), 3);
         if (const char *e = getenv("RT_WIDE_OPTS")) sscanf(e, "%d,%d,%d", &budget, &batch, &stop);   // tools: A/B
         split = (RT_WIDE_PERSIST ? sp : 0) | (std::min(std::max(budget, 1), 255) << 8) |
                 (std::min(std::max(batch, 0), 64) << 16) | (std::min(std::max(stop, 0), 64) << 24);

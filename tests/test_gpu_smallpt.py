@@ -162,6 +162,37 @@ def test_configs4_full_size_golden(rt, oracle, counted, walk, monkeypatch):
         assert f.counters[3] == w * h * 64
 
 
+@pytest.mark.parametrize("heavy", [None, "4096"])
+@pytest.mark.parametrize("counted", [False, True])
+def test_configs4_cooperative_walk_golden(rt, oracle, counted, heavy, monkeypatch):
+    """The heaviest tiles walk the 8-wide hierarchy eight lanes per pixel
+    (wide_walk_coop) once a learnt order exists: the 1st frame of a key
+    records the tile costs, the 3rd dispatches the heavy tiles cooperatively.
+    Every frame must equal the reference core's golden hashes (configs[4],
+    1920x1080, 64 spp), counted (and the counters exact) and uncounted, with
+    the default number of cooperative tiles and with 4096 of them."""
+    import json
+    import os
+    monkeypatch.setenv("RT_SPT_SPLIT", "3")
+    if heavy:
+        monkeypatch.setenv("RT_WIDE_HEAVY", heavy)
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
+    g = gold["smallpt"]["1920x1080_64spp_complex10k"]
+    spheres, n, cam = rt.scenes.complex10k()
+    w, h = 1920, 1080
+    rt.scenes.update_camera(cam, w, h)
+    first = None
+    for _ in range(3):
+        f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n, camera=cam)
+        f.render(64, counters=counted)
+        got = (oracle.fnv1a64(f.colors), oracle.fnv1a64(f.pixels), oracle.fnv1a64(f.seeds))
+        assert got == (g["colors"], g["pixels"], g["seeds"])
+        if counted:                      # the 1st frame (no order yet) walks a lane per pixel
+            assert f.counters[3] == w * h * 64
+            first = first or list(f.counters)
+            assert list(f.counters) == first
+
+
 def test_async_device_paths(rt, oracle):
     """spt_scene_render_async and spt_render_async on device buffers, rows
     split in two calls, seeds_in != seeds_out."""
