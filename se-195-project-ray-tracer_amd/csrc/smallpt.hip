@@ -844,39 +844,57 @@ __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigne
 // the reference's: every sphere a per-lane walk would test is tested with
 // the same float formula, and the nearest hit is the minimum distance with
 // the highest reference index on ties, an order-independent choice.
+// G = 4 (COOP4): four lanes per pixel, two child slots / spheres per lane --
+// half the waves per heavy tile for a somewhat longer trip.
 __device__ __forceinline__ int dpp_xor1(int v) { return __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false); }
 __device__ __forceinline__ int dpp_xor2(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false); }
 __device__ __forceinline__ int dpp_mir8(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false); }
-__device__ __forceinline__ float grp8_min(float v)
+template <int G>
+__device__ __forceinline__ float grp_min(float v)
 {
     v = fminf(v, __int_as_float(dpp_xor1(__float_as_int(v))));
     v = fminf(v, __int_as_float(dpp_xor2(__float_as_int(v))));
-    return fminf(v, __int_as_float(dpp_mir8(__float_as_int(v))));
+    if (G == 8) v = fminf(v, __int_as_float(dpp_mir8(__float_as_int(v))));
+    return v;
 }
-__device__ __forceinline__ int grp8_max(int v)
+template <int G>
+__device__ __forceinline__ int grp_max(int v)
 {
     v = max(v, dpp_xor1(v));
     v = max(v, dpp_xor2(v));
-    return max(v, dpp_mir8(v));
+    if (G == 8) v = max(v, dpp_mir8(v));
+    return v;
 }
-// The group's 8 bits of a predicate (bit k = lane 8g + k).
-__device__ __forceinline__ unsigned grp8_bits(bool p, int gbase)
+// The group's G bits of a predicate (bit k = lane gbase + k).
+template <int G>
+__device__ __forceinline__ unsigned grp_bits(bool p, int gbase)
 {
-    return (unsigned)(__builtin_amdgcn_ballot_w64(p) >> gbase) & 255u;
+    return (unsigned)(__builtin_amdgcn_ballot_w64(p) >> gbase) & ((1u << G) - 1u);
 }
 
-// wide_visit for one child slot per lane: lane k of the group tests slot
-// k ^ oct and the group's visit mask (bit k) comes back from a ballot.  The
-// float operations are wide_visit's, so the culling decisions are its own.
+// wide_visit split over the group: lane k tests the child at visit
+// positions k, k + G, ... (slot position ^ oct) and the group's visit mask
+// comes back from ballots.  The float operations are wide_visit's, so the
+// culling decisions are its own.
+template <int G>
 __device__ __forceinline__ unsigned wide_visit_coop(const uint4 *__restrict__ N, const ray3 &r, float ix, float iy,
                                                     float iz, float alpha, int oct, float lim, int pos, int gbase,
-                                                    const unsigned *__restrict__ hid = nullptr, int idmin = -1)
+                                                    unsigned &lm, const unsigned *__restrict__ hid = nullptr,
+                                                    int idmin = -1)
 {
     const uint4 h0 = N[0];
     const float2 h1 = *(const float2 *)(N + 1);
-    const int sl = pos ^ oct;
-    const unsigned *q = (const unsigned *)N + 16 + 6 * (sl >> 2);
-    const uint2 w0 = *(const uint2 *)q, w1 = *(const uint2 *)(q + 2), w2 = *(const uint2 *)(q + 4);
+    uint2 w[8 / G][3];
+    int cwk[8 / G];                       // this lane's children's words (< 0: a leaf)
+#pragma unroll
+    for (int j = 0; j < 8 / G; j++) cwk[j] = (int)((const unsigned *)N)[8 + ((pos + j * G) ^ oct)];
+#pragma unroll
+    for (int j = 0; j < 8 / G; j++) {
+        const unsigned *q = (const unsigned *)N + 16 + 6 * (((pos + j * G) ^ oct) >> 2);
+        w[j][0] = *(const uint2 *)q;
+        w[j][1] = *(const uint2 *)(q + 2);
+        w[j][2] = *(const uint2 *)(q + 4);
+    }
     const float cx = __uint_as_float(h0.x) - r.o.x, cy = __uint_as_float(h0.y) - r.o.y,
                 cz = __uint_as_float(h0.z) - r.o.z;
     const float dist = __builtin_amdgcn_sqrtf(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, cz * cz)));
@@ -887,85 +905,161 @@ __device__ __forceinline__ unsigned wide_visit_coop(const uint4 *__restrict__ N,
     const float bx = cx * ix, by = cy * iy, bz = cz * iz;
     const float mx = m * fabsf(ix), my = m * fabsf(iy), mz = m * fabsf(iz);
     const float bnx = bx - mx, bfx = bx + mx, bny = by - my, bfy = by + my, bnz = bz - mz, bfz = bz + mz;
-    const unsigned lx = w0.x, ly = w0.y, lz = w1.x, ux = w1.y, uy = w2.x, uz = w2.y;
-    const unsigned nxw = (oct & 1) ? ux : lx, fxw = (oct & 1) ? lx : ux;
-    const unsigned nyw = (oct & 2) ? uy : ly, fyw = (oct & 2) ? ly : uy;
-    const unsigned nzw = (oct & 4) ? uz : lz, fzw = (oct & 4) ? lz : uz;
-    const int sh = 8 * (sl & 3);
-    const float tnx = __builtin_fmaf((float)((nxw >> sh) & 255u), ax, bnx);
-    const float tfx = __builtin_fmaf((float)((fxw >> sh) & 255u), ax, bfx);
-    const float tny = __builtin_fmaf((float)((nyw >> sh) & 255u), ay, bny);
-    const float tfy = __builtin_fmaf((float)((fyw >> sh) & 255u), ay, bfy);
-    const float tnz = __builtin_fmaf((float)((nzw >> sh) & 255u), az, bnz);
-    const float tfz = __builtin_fmaf((float)((fzw >> sh) & 255u), az, bfz);
-    const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.f));
-    const float tf = fminf(fminf(tfx, tfy), fminf(tfz, lim));
-    bool hit = tn <= tf && ((h0.w >> (24 + sl)) & 1u);
-    if (hid && idmin >= 0) hit = hit && (int)hid[sl] > idmin;
-    return grp8_bits(hit, gbase);
+    unsigned hm = 0;
+    lm = 0;
+#pragma unroll
+    for (int j = 0; j < 8 / G; j++) {
+        const int sl = (pos + j * G) ^ oct;
+        const unsigned lx = w[j][0].x, ly = w[j][0].y, lz = w[j][1].x, ux = w[j][1].y, uy = w[j][2].x,
+                       uz = w[j][2].y;
+        const unsigned nxw = (oct & 1) ? ux : lx, fxw = (oct & 1) ? lx : ux;
+        const unsigned nyw = (oct & 2) ? uy : ly, fyw = (oct & 2) ? ly : uy;
+        const unsigned nzw = (oct & 4) ? uz : lz, fzw = (oct & 4) ? lz : uz;
+        const int sh = 8 * (sl & 3);
+        const float tnx = __builtin_fmaf((float)((nxw >> sh) & 255u), ax, bnx);
+        const float tfx = __builtin_fmaf((float)((fxw >> sh) & 255u), ax, bfx);
+        const float tny = __builtin_fmaf((float)((nyw >> sh) & 255u), ay, bny);
+        const float tfy = __builtin_fmaf((float)((fyw >> sh) & 255u), ay, bfy);
+        const float tnz = __builtin_fmaf((float)((nzw >> sh) & 255u), az, bnz);
+        const float tfz = __builtin_fmaf((float)((fzw >> sh) & 255u), az, bfz);
+        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.f));
+        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, lim));
+        bool hit = tn <= tf && ((h0.w >> (24 + sl)) & 1u);
+        if (hid && idmin >= 0) hit = hit && (int)hid[sl] > idmin;
+        hm |= grp_bits<G>(hit, gbase) << (j * G);
+        lm |= grp_bits<G>(hit && cwk[j] < 0, gbase) << (j * G);
+    }
+    return hm;
 }
 
-// One leaf (first sphere f, c spheres) for the group: sphere b + k on lane k.
-// Nearest hit: t / bpos updated to the minimum distance, highest reference
-// index on ties (ids loaded only then).  Any hit: COUNT -- id = the highest
-// occluder index so far; otherwise bpos = f marks "occluded" and the caller
-// ends the walk.
-template <bool COUNT>
-__device__ __forceinline__ void leaf_coop(const BvhView &B, const ray3 &r, bool shadow, float maxt, int f, int c,
-                                          int pos, int gbase, float &t, int &bpos, int &id)
+// Applies one leaf pass's distances d[j] (sphere b + pos + j G of the leaf
+// at f; MISS past its end) to the group's query.  Nearest hit: t / bpos
+// updated to the minimum distance, highest reference index on ties (ids
+// loaded only then).  Any hit: COUNT -- id = the highest occluder index so
+// far; otherwise returns true (occluded: bpos = f) and the caller ends the walk.
+template <bool COUNT, int G>
+__device__ __forceinline__ bool leaf_apply(const BvhView &B, bool shadow, float maxt, int f, int b, int pos,
+                                           int gbase, const float (&d)[8 / G], float &t, int &bpos, int &id)
 {
-    for (int b = 0; b < c; b += 8) {
-        const int q = b + pos;
-        const bool have = q < c;
-        const float4 g = B.geo[f + (have ? q : 0)];
-        const float opx = g.x - r.o.x, opy = g.y - r.o.y, opz = g.z - r.o.z;
-        const float bb = opx * r.d.x + opy * r.d.y + opz * r.d.z;
-        const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g.w;
-        float d;
-        if (wave_any(have && fabsf(det) < 0x1p-96f)) {
-            d = sphere_hit(g, r);
-        } else {
-            const float sd = sqrt_nr(det);
-            const float t1 = bb - sd, t2 = bb + sd;
-            d = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
+    constexpr int S = 8 / G;
+    if (shadow) {
+        bool occ[S];
+        unsigned any = 0;
+#pragma unroll
+        for (int j = 0; j < S; j++) {
+            occ[j] = d[j] < maxt;
+            any |= grp_bits<G>(occ[j], gbase);
         }
-        if (!have) d = MISS;
-        if (shadow) {
-            const bool occ = d < maxt;
-            if (COUNT) {
+        if (COUNT) {
+            if (any) {
                 int i = -1;
-                if (grp8_bits(occ, gbase)) {
-                    if (occ) i = B.id[f + q];
-                    i = grp8_max(i);
-                }
+#pragma unroll
+                for (int j = 0; j < S; j++)
+                    if (occ[j]) i = max(i, B.id[f + b + pos + j * G]);
+                i = grp_max<G>(i);
                 if (i > id) id = i;
-            } else if (grp8_bits(occ, gbase)) {
-                bpos = f;
-                return;
             }
-        } else {
-            const float dm = grp8_min(d);
-            if (dm <= t) {                      // (dm finite: t < +inf)
-                const unsigned cm = grp8_bits(d == dm, gbase);
-                if (dm < t && __builtin_popcount(cm) == 1) {
-                    t = dm;
-                    bpos = f + b + __builtin_ctz(cm);
-                } else {                        // a tie: within the leaf, or with the best so far
-                    int i = -1;
-                    if (d == dm) i = B.id[f + q];
-                    const int im = grp8_max(i);
-                    const int cur_id = dm == t ? (bpos >= 0 ? B.id[bpos] : id) : -1;
-                    if (im > cur_id) {
-                        t = dm;
-                        bpos = f + b + __builtin_ctz(grp8_bits(i == im, gbase));
-                    }
+        } else if (any) {
+            bpos = f;
+            return true;
+        }
+        return false;
+    }
+    float dl = d[0];
+#pragma unroll
+    for (int j = 1; j < S; j++) dl = fminf(dl, d[j]);
+    const float dm = grp_min<G>(dl);
+    if (dm <= t) {                              // (dm finite: t < +inf)
+        unsigned cm[S];
+        int nc = 0;
+#pragma unroll
+        for (int j = 0; j < S; j++) {
+            cm[j] = grp_bits<G>(d[j] == dm, gbase);
+            nc += __builtin_popcount(cm[j]);
+        }
+        if (dm < t && nc == 1) {
+            int k = 0;
+#pragma unroll
+            for (int j = 0; j < S; j++)
+                if (cm[j]) k = j * G + __builtin_ctz(cm[j]);
+            t = dm;
+            bpos = f + b + k;
+        } else {                                // a tie: within the leaf, or with the best so far
+            int il[S], i = -1;
+#pragma unroll
+            for (int j = 0; j < S; j++) {
+                il[j] = d[j] == dm ? B.id[f + b + pos + j * G] : -1;
+                i = max(i, il[j]);
+            }
+            const int im = grp_max<G>(i);
+            const int cur_id = dm == t ? (bpos >= 0 ? B.id[bpos] : id) : -1;
+            if (im > cur_id) {
+                int k = 0;
+#pragma unroll
+                for (int j = 0; j < S; j++) {
+                    const unsigned wm = grp_bits<G>(il[j] == im, gbase);
+                    if (wm) k = j * G + __builtin_ctz(wm);
                 }
+                t = dm;
+                bpos = f + b + k;
             }
         }
     }
+    return false;
 }
 
-template <bool COUNT>
+// Up to NL leaves (first sphere f[l], c[l] spheres; c = 0: none) for the
+// group, sphere b + k + j G of each on lane k: the sphere loads of all of
+// them are issued before the first test (one memory latency per pass), the
+// leaves then applied in order.  Returns true when an uncounted any-hit
+// found an occluder.
+template <bool COUNT, int G, int NL>
+__device__ __forceinline__ bool leaf_coop(const BvhView &B, const ray3 &r, bool shadow, float maxt,
+                                          const int (&f)[NL], const int (&c)[NL], int pos, int gbase, float &t,
+                                          int &bpos, int &id)
+{
+    constexpr int S = 8 / G;
+    int cmax = c[0];
+#pragma unroll
+    for (int l = 1; l < NL; l++) cmax = max(cmax, c[l]);
+    for (int b = 0; b < cmax; b += 8) {
+        float4 g[NL][S];
+#pragma unroll
+        for (int l = 0; l < NL; l++)
+#pragma unroll
+            for (int j = 0; j < S; j++) {
+                const int q = b + pos + j * G;
+                g[l][j] = B.geo[f[l] + (q < c[l] ? q : 0)];
+            }
+#pragma unroll
+        for (int l = 0; l < NL; l++) {
+            if (b >= c[l]) continue;
+            float d[S];
+            bool bad = false;
+#pragma unroll
+            for (int j = 0; j < S; j++) {
+                const float opx = g[l][j].x - r.o.x, opy = g[l][j].y - r.o.y, opz = g[l][j].z - r.o.z;
+                const float bb = opx * r.d.x + opy * r.d.y + opz * r.d.z;
+                const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g[l][j].w;
+                bad = bad || (b + pos + j * G < c[l] && fabsf(det) < 0x1p-96f);
+                const float sd = sqrt_nr(det);
+                const float t1 = bb - sd, t2 = bb + sd;
+                d[j] = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
+            }
+            if (wave_any(bad)) {
+#pragma unroll
+                for (int j = 0; j < S; j++) d[j] = sphere_hit(g[l][j], r);
+            }
+#pragma unroll
+            for (int j = 0; j < S; j++)
+                if (b + pos + j * G >= c[l]) d[j] = MISS;
+            if (leaf_apply<COUNT, G>(B, shadow, maxt, f[l], b, pos, gbase, d, t, bpos, id)) return true;
+        }
+    }
+    return false;
+}
+
+template <bool COUNT, int G>
 __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, unsigned *__restrict__ stk,
                                const ray3 &r, bool shadow, BvhWalk &W, int opts)
 {
@@ -984,7 +1078,7 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
     const unsigned *Lw = (const unsigned *)L;
     const unsigned *Lmax = COUNT ? (const unsigned *)(L + 7 * B.wnodes) : nullptr;
     unsigned *my = stk + (threadIdx.x & 63);
-    const int pos = threadIdx.x & 7, gbase = threadIdx.x & 56;
+    const int pos = threadIdx.x & (G - 1), gbase = threadIdx.x & (64 - G);
     const int n0 = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true));
     int trips = 0;
     while (true) {
@@ -998,25 +1092,52 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
                 m &= m - 1;
                 cw = (int)Lw[cur * WIDE_WORDS + 8 + (p ^ oct)];
             }
-            if (cw < 0) {
+            if (cw < 0) {                       // (a root leaf: child leaves are tested at their parent)
                 const int lf = ~cw;
-                leaf_coop<COUNT>(B, r, shadow, maxt, lf & 0xffffff, lf >> 24, pos, gbase, t, bpos, id);
-                if (!COUNT && shadow && bpos >= 0) {
+                const int fa[1] = {lf & 0xffffff}, ca[1] = {lf >> 24};
+                if (leaf_coop<COUNT, G, 1>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id)) {
                     m = 0;
                     sp = 0;
                 }
             } else {
+                unsigned lm;
                 const unsigned hm =
-                    COUNT ? wide_visit_coop(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase,
-                                            Lmax + 8 * cw, shadow ? id : -1)
-                          : wide_visit_coop(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase);
-                if (hm) {
+                    COUNT ? wide_visit_coop<G>(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase,
+                                               lm, Lmax + 8 * cw, shadow ? id : -1)
+                          : wide_visit_coop<G>(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase,
+                                               lm);
+                // The node's crossed leaves at once, two per pass (their
+                // sphere loads in flight together), before its inner children.
+                bool occl = false;
+                unsigned l = lm;
+                while (l) {
+                    const int i0 = __builtin_ctz(l);
+                    l &= l - 1;
+                    const int w0 = ~(int)Lw[cw * WIDE_WORDS + 8 + (i0 ^ oct)];
+                    int fa[2] = {w0 & 0xffffff, 0}, ca[2] = {w0 >> 24, 0};
+                    if (l) {
+                        const int i1 = __builtin_ctz(l);
+                        l &= l - 1;
+                        const int w1 = ~(int)Lw[cw * WIDE_WORDS + 8 + (i1 ^ oct)];
+                        fa[1] = w1 & 0xffffff;
+                        ca[1] = w1 >> 24;
+                    }
+                    if (leaf_coop<COUNT, G, 2>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id)) {
+                        occl = true;
+                        break;
+                    }
+                }
+                const unsigned nm = hm & ~lm;
+                if (occl) {
+                    m = 0;
+                    sp = 0;
+                } else if (nm) {
                     if (m) {
                         my[64 * sp] = ((unsigned)cur << 8) | m;
                         sp++;
                     }
                     cur = cw;
-                    m = hm;
+                    m = nm;
                 }
             }
             if (m == 0 && sp > 0) {
@@ -1106,6 +1227,9 @@ constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2, GEO_WIDE = 3;
 #endif
 #ifndef RT_WIDE_MINWAVES
 #define RT_WIDE_MINWAVES 4  // the 8-wide (LDS) hierarchy kernels: 126 VGPRs unbounded; 5 or 6 waves per SIMD spill
+#endif
+#ifndef RT_SPT_COOP_G
+#define RT_SPT_COOP_G 8     // lanes per pixel of the cooperative walk (heavy tiles of the 8-wide kernels): 8 or 4
 #endif
 #ifndef RT_SPT_GSTORE
 #define RT_SPT_GSTORE 1     // hierarchy kernels: a group's outputs stored whole by its last wave (A/B: 0)
@@ -1201,6 +1325,8 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // on several SIMDs), f = (nheavy << hs) + ... the rest whole.
     // (split: hs in bits 0..1; the wide walk's options above them, wide_walk)
     const int hs = PERSIST ? (split & 3) : 0;
+    // waves of a block that take heavy sub-items first (split bits 3..7; 0: 4 << hs)
+    const int hw = ((split >> 3) & 31) ? ((split >> 3) & 31) : (4 << hs);
     const int nitems = 4 * ((ntiles + 3) >> 2);
     const int nh = PERSIST ? min(nheavy, nitems) : 0;
     const int nwork = (nh << hs) + (nitems - nh);
@@ -1213,7 +1339,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         int v = 0;
         if (lane == 0) {
             v = -1;
-            if (wave < (4 << hs) && nh > 0) {
+            if (wave < hw && nh > 0) {
                 const int hv = atomicAdd(work + 1, 1);
                 if (hv < (nh << hs)) v = hv;
             }
@@ -1225,20 +1351,22 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     if (PERSIST) f = __builtin_amdgcn_readfirstlane(fetch());
     while (!PERSIST || f < nwork) {
     const bool heavy_ = f < (nh << hs);
-    // hs = 3 (COOP): a heavy tile's 8 sub-items are 8 rows of 8 pixels with
-    // eight lanes per pixel (lane group g = pixel g of the row), walking the
-    // hierarchy cooperatively (wide_walk_coop).  Otherwise a sub-item is
-    // 64 >> hs pixels, a lane each.
-    const bool coop = GEO == GEO_WIDE && heavy_ && hs == 3;
+    // hs = 3 (COOP, G = 8): a heavy tile's 8 sub-items are 8 rows of 8 pixels
+    // with eight lanes per pixel (lane group g = pixel g of the row), walking
+    // the hierarchy cooperatively (wide_walk_coop); hs = 2 with split bit 2
+    // (G = 4): 4 sub-items of 16 pixels, four lanes per pixel.  Otherwise a
+    // sub-item is 64 >> hs pixels, a lane each.
+    const int cg = (GEO == GEO_WIDE && heavy_ && hs == (RT_SPT_COOP_G == 8 ? 3 : 2) && (split & 4)) ? RT_SPT_COOP_G : 0;
+    const bool coop = cg != 0;
     const int sp_ = heavy_ && !coop ? hs : 0;
     const int item = heavy_ ? f >> hs : f - (nh << hs) + nh;
     const int sub = heavy_ ? f & ((1 << hs) - 1) : 0;
     const int slot = item >> 2;
     const int grp = (SCHED && group_order) ? group_order[slot] : slot;
     const int tile = grp * 4 + (item & 3);
-    const int li = coop ? (sub << 3) + (lane >> 3)      // pixel of the 8x8 tile (valid: lane < 64 >> split)
-                        : (sub << (6 - sp_)) + lane;
-    const bool lead = !coop || (lane & 7) == 0;         // the lane that stores the pixel and counts
+    const int li = coop ? (sub << (6 - hs)) + (cg == 8 ? lane >> 3 : lane >> 2)   // pixel of the 8x8 tile
+                        : (sub << (6 - sp_)) + lane;    //   (valid: lane < 64 >> split)
+    const bool lead = !coop || (lane & (cg - 1)) == 0;  // the lane that stores the pixel and counts
     unsigned long long t_start = 0;
     if (SCHED) t_start = __builtin_amdgcn_s_memrealtime();
     // GSTORE (hierarchy kernels): per group of the block a 32x8 staging
@@ -1444,7 +1572,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 tr_queries += !walking;
 #endif
                 if (!walking) wide_begin<COUNT>(bvh, ray, shadow, t, walk);
-                walking = coop ? !wide_walk_coop<COUNT>(bvh, wL, wstk, ray, shadow, walk, split)
+                walking = coop ? !wide_walk_coop<COUNT, RT_SPT_COOP_G>(bvh, wL, wstk, ray, shadow, walk, split)
                                : !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
 #ifdef RT_SPT_TRACE
                 tr_walk += (unsigned)(__builtin_amdgcn_s_memtime() - tr_w0);
@@ -1780,7 +1908,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         }
     }
 #endif
-    if (COUNT && PERSIST && hs == 3) {                  // a cooperative group counts its pixel once:
+    if (COUNT && PERSIST && (split & 4)) {              // a cooperative group counts its pixel once:
         if (!lead) cnt = Counts{0, 0, 0, 0};            //   flushed per work item
         const unsigned long long c[4] = {cnt.isect, cnt.isectp, cnt.tests, cnt.samples};
         flush_counters<4>(counters, c);
@@ -1980,8 +2108,10 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     int split = 0;
     if (GEO == rt::smallpt::GEO_WIDE) {
         int sp = 0, budget = RT_WIDE_BUDGET, batch = RT_BVH_BATCH, stop = RT_WIDE_STOP;
-        // heavy tiles split 2^k ways (A/B), k = 3: 8 lanes per pixel (wide_walk_coop)
+        // heavy tiles split 2^k ways (A/B); 3: RT_SPT_COOP_G lanes per pixel (wide_walk_coop)
         if (const char *e = getenv("RT_SPT_SPLIT")) sp = std::min(std::max(atoi(e), 0), 3);
+        if (sp == 3) sp = (RT_SPT_COOP_G == 8 ? 3 : 2) | 4;
+        if (const char *e = getenv("RT_WIDE_HEAVY_WAVES")) sp |= std::min(std::max(atoi(e), 0), 16) << 3;   // A/B
         if (const char *e = getenv("RT_WIDE_OPTS")) sscanf(e, "%d,%d,%d", &budget, &batch, &stop);   // tools: A/B
         split = (RT_WIDE_PERSIST ? sp : 0) | (std::min(std::max(budget, 1), 255) << 8) |
                 (std::min(std::max(batch, 0), 64) << 16) | (std::min(std::max(stop, 0), 64) << 24);
