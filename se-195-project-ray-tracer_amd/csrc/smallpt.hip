@@ -2100,18 +2100,36 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
         work = sc.d_work + 2 * (sc.work_next++ % spt_scene::NWORK);
         if (hipMemsetAsync(work, 0, 2 * sizeof(int), s) != hipSuccess) return;   // (check_launch reports it)
     }
-    int nheavy = 0;                   // with a learnt order: one heavy tile per SIMD of the grid first
+    // Heavy tiles (with a learnt order, GEO_WIDE persistent launches): the
+    // first nheavy tiles in dispatch order.  A window of many waves per SIMD
+    // (a full frame: 31.6) runs one heavy tile per SIMD beside lighter
+    // waves; a window of few (a multi-GPU rank's share: N = 8 is 4.0, N = 4
+    // 7.9) is bound by its heaviest tiles' sample chains, so the heaviest 512
+    // (per 256 CUs) walk cooperatively, RT_SPT_COOP_G lanes per pixel
+    // (wide_walk_coop), fetched first by every wave of a block (N = 8) or by
+    // half of them (N = 4).  configs[4], 64 spp (profiles/r03/c4_coop_*.log):
+    // N = 8 windows 18.0-19.8 -> 11.4-14.8 ms, N = 4 18.7 -> 16.9 ms; the
+    // full frame and N = 2 lose with it (28.2 -> 29-31 ms, 21.1 -> 23-24 ms).
+    int nheavy = 0, sp = 0;
     if (GEO == rt::smallpt::GEO_WIDE && RT_WIDE_PERSIST && g.order) {
         nheavy = std::min(4 * g.nblocks, 4 * g.nslots);
+        const double wps = (double)g.ntiles / (4.0 * sc.cus);
+        if (wps <= 10.0) {
+            nheavy = std::min(2 * sc.cus, 4 * g.nslots);
+            sp = (RT_SPT_COOP_G == 8 ? 3 : 2) | 4 | ((wps <= 5.0 ? 16 : 8) << 3);
+        }
         if (const char *e = getenv("RT_WIDE_HEAVY")) nheavy = std::min(std::max(atoi(e), 0), 4 * g.nslots);   // A/B
     }
     int split = 0;
     if (GEO == rt::smallpt::GEO_WIDE) {
-        int sp = 0, budget = RT_WIDE_BUDGET, batch = RT_BVH_BATCH, stop = RT_WIDE_STOP;
-        // heavy tiles split 2^k ways (A/B); 3: RT_SPT_COOP_G lanes per pixel (wide_walk_coop)
-        if (const char *e = getenv("RT_SPT_SPLIT")) sp = std::min(std::max(atoi(e), 0), 3);
-        if (sp == 3) sp = (RT_SPT_COOP_G == 8 ? 3 : 2) | 4;
-        if (const char *e = getenv("RT_WIDE_HEAVY_WAVES")) sp |= std::min(std::max(atoi(e), 0), 16) << 3;   // A/B
+        int budget = RT_WIDE_BUDGET, batch = RT_BVH_BATCH, stop = RT_WIDE_STOP;
+        // A/B: heavy tiles split 2^k ways (k = 0..2: a lane per pixel), 3: cooperative
+        if (const char *e = getenv("RT_SPT_SPLIT")) {
+            sp = std::min(std::max(atoi(e), 0), 3);
+            if (sp == 3) sp = (RT_SPT_COOP_G == 8 ? 3 : 2) | 4;
+        }
+        if (const char *e = getenv("RT_WIDE_HEAVY_WAVES"))   // A/B: waves per block taking heavy items first
+            sp = (sp & 7) | (std::min(std::max(atoi(e), 0), 16) << 3);
         if (const char *e = getenv("RT_WIDE_OPTS")) sscanf(e, "%d,%d,%d", &budget, &batch, &stop);   // tools: A/B
         split = (RT_WIDE_PERSIST ? sp : 0) | (std::min(std::max(budget, 1), 255) << 8) |
                 (std::min(std::max(batch, 0), 64) << 16) | (std::min(std::max(stop, 0), 64) << 24);

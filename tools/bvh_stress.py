@@ -6,6 +6,7 @@ rendered with the hierarchy and with the full scan (RT_SPT_NO_BVH) and
 compared bit for bit (colours, seeds, pixels, work counters).
 
     N=60 python tools/bvh_stress.py
+    REPEAT=3 RT_SPT_SPLIT=3 N=60 python tools/bvh_stress.py   # learnt order: cooperative heavy tiles
 """
 import os
 import sys
@@ -68,7 +69,7 @@ def main():
         S, n, cam, desc = scene(rng)
         mode = int(rng.integers(0, 2))
         ref = render(S, n, cam, mode, True, True)
-        for counted in (True, False):
+        for counted in [True, False] * int(os.environ.get("REPEAT", "1")):
             f = render(S, n, cam, mode, False, counted)
             same = (np.array_equal(f.colors.view(np.uint32), ref.colors.view(np.uint32))
                     and np.array_equal(f.seeds, ref.seeds) and np.array_equal(f.pixels, ref.pixels)
