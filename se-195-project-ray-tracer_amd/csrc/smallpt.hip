@@ -645,6 +645,9 @@ __device__ __forceinline__ unsigned wide_visit(const uint4 *__restrict__ N, cons
     return hm;
 }
 
+#ifndef RT_SPT_COOP_NL
+#define RT_SPT_COOP_NL 2    // cooperative walk: leaves tested per pass (loads in flight together)
+#endif
 #ifndef RT_WIDE_BUDGET
 #define RT_WIDE_BUDGET 16   // wide-walk trips per render-loop iteration before a lane's query is suspended
 #endif
@@ -1106,23 +1109,25 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
                                                lm, Lmax + 8 * cw, shadow ? id : -1)
                           : wide_visit_coop<G>(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase,
                                                lm);
-                // The node's crossed leaves at once, two per pass (their
-                // sphere loads in flight together), before its inner children.
+                // The node's crossed leaves at once, RT_SPT_COOP_NL per pass
+                // (their words read and their sphere loads issued together),
+                // before its inner children.
                 bool occl = false;
                 unsigned l = lm;
                 while (l) {
-                    const int i0 = __builtin_ctz(l);
-                    l &= l - 1;
-                    const int w0 = ~(int)Lw[cw * WIDE_WORDS + 8 + (i0 ^ oct)];
-                    int fa[2] = {w0 & 0xffffff, 0}, ca[2] = {w0 >> 24, 0};
-                    if (l) {
-                        const int i1 = __builtin_ctz(l);
-                        l &= l - 1;
-                        const int w1 = ~(int)Lw[cw * WIDE_WORDS + 8 + (i1 ^ oct)];
-                        fa[1] = w1 & 0xffffff;
-                        ca[1] = w1 >> 24;
+                    int fa[RT_SPT_COOP_NL], ca[RT_SPT_COOP_NL];
+#pragma unroll
+                    for (int q = 0; q < RT_SPT_COOP_NL; q++) {
+                        fa[q] = ca[q] = 0;
+                        if (l) {
+                            const int iq = __builtin_ctz(l);
+                            l &= l - 1;
+                            const int wq = ~(int)Lw[cw * WIDE_WORDS + 8 + (iq ^ oct)];
+                            fa[q] = wq & 0xffffff;
+                            ca[q] = wq >> 24;
+                        }
                     }
-                    if (leaf_coop<COUNT, G, 2>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id)) {
+                    if (leaf_coop<COUNT, G, RT_SPT_COOP_NL>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id)) {
                         occl = true;
                         break;
                     }
