@@ -1330,32 +1330,41 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // on several SIMDs), f = (nheavy << hs) + ... the rest whole.
     // (split: hs in bits 0..1; the wide walk's options above them, wide_walk)
     const int hs = PERSIST ? (split & 3) : 0;
-    // waves of a block that take heavy sub-items first (split bits 3..7; 0: 4 << hs)
+    // waves of a block that take tier-1 sub-items first (split bits 3..7; 0: 4 << hs)
     const int hw = ((split >> 3) & 31) ? ((split >> 3) & 31) : (4 << hs);
     const int nitems = 4 * ((ntiles + 3) >> 2);
-    const int nh = PERSIST ? min(nheavy, nitems) : 0;
-    const int nwork = (nh << hs) + (nitems - nh);
-    // Persistent fetch: waves 0..(4 << hs) - 1 of a block -- 1 << hs per SIMD
-    // -- take the heavy sub-items first (work[1]), the others, and those once
-    // the heavy ones are gone, the rest in order (work[0]): a heavy tile's
-    // SIMD shares its issue slots with lighter, lower-priority waves instead
-    // of with three other heavy tiles.
+    // Three tiers, in dispatch order (heaviest first with a learnt order):
+    // nheavy bits 0..15 = n1 tiles split into 2^hs sub-items each (the
+    // cooperative walk with split bit 2), bits 16..31 = n2 tiles routed one
+    // per SIMD, then the rest.
+    const int n1 = PERSIST ? min(nheavy & 0xffff, nitems) : 0;
+    const int n2 = PERSIST ? min((nheavy >> 16) & 0xffff, nitems - n1) : 0;
+    const int nwork = (n1 << hs) + (nitems - n1);
+    // Persistent fetch: waves 0..hw - 1 of a block take tier-1 sub-items
+    // first (work[2]); waves 0..3 -- one per SIMD -- then take tier-2 tiles
+    // (work[1]): a heavy tile's SIMD shares its issue slots with lighter,
+    // lower-priority waves instead of with three other heavy tiles; every
+    // wave then takes the rest in order (work[0]).
     const auto fetch = [&]() {
         int v = 0;
         if (lane == 0) {
             v = -1;
-            if (wave < hw && nh > 0) {
-                const int hv = atomicAdd(work + 1, 1);
-                if (hv < (nh << hs)) v = hv;
+            if (wave < hw && n1 > 0) {
+                const int hv = atomicAdd(work + 2, 1);
+                if (hv < (n1 << hs)) v = hv;
             }
-            if (v < 0) v = (nh << hs) + atomicAdd(work, 1);
+            if (v < 0 && wave < 4 && n2 > 0) {
+                const int hv = atomicAdd(work + 1, 1);
+                if (hv < n2) v = (n1 << hs) + hv;
+            }
+            if (v < 0) v = (n1 << hs) + n2 + atomicAdd(work, 1);
         }
         return __shfl(v, 0, 64);
     };
     int f = ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) * 4 + (wave & 3);
     if (PERSIST) f = __builtin_amdgcn_readfirstlane(fetch());
     while (!PERSIST || f < nwork) {
-    const bool heavy_ = f < (nh << hs);
+    const bool heavy_ = f < (n1 << hs);
     // hs = 3 (COOP, G = 8): a heavy tile's 8 sub-items are 8 rows of 8 pixels
     // with eight lanes per pixel (lane group g = pixel g of the row), walking
     // the hierarchy cooperatively (wide_walk_coop); hs = 2 with split bit 2
@@ -1364,7 +1373,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     const int cg = (GEO == GEO_WIDE && heavy_ && hs == (RT_SPT_COOP_G == 8 ? 3 : 2) && (split & 4)) ? RT_SPT_COOP_G : 0;
     const bool coop = cg != 0;
     const int sp_ = heavy_ && !coop ? hs : 0;
-    const int item = heavy_ ? f >> hs : f - (nh << hs) + nh;
+    const int item = heavy_ ? f >> hs : f - (n1 << hs) + n1;
     const int sub = heavy_ ? f & ((1 << hs) - 1) : 0;
     const int slot = item >> 2;
     const int grp = (SCHED && group_order) ? group_order[slot] : slot;
@@ -2001,8 +2010,8 @@ struct spt_scene {
     bool force_global = false;        // RT_SPT_GEO=global: scalar-load path at any size (A/B)
     mutable SptSched sched;           // adaptive group order (hierarchy scenes)
     // Work counters of the persistent (8-wide hierarchy) launches: a ring,
-    // one zeroed pair (in order, heavy) per launch, so launches in flight on
-    // several streams do not share one.
+    // one zeroed quad (rest, routed heavy, cooperative, unused) per launch, so
+    // launches in flight on several streams do not share one.
     static constexpr int NWORK = 64;
     int *d_work = nullptr;
     mutable int work_next = 0;
@@ -2102,39 +2111,47 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     int *work = nullptr;
     if (GEO == rt::smallpt::GEO_WIDE) {
         lds = wide_lds_bytes(sc.bvh.wnodes, sc.bvh.wdepth, g.wpb, COUNT);
-        work = sc.d_work + 2 * (sc.work_next++ % spt_scene::NWORK);
-        if (hipMemsetAsync(work, 0, 2 * sizeof(int), s) != hipSuccess) return;   // (check_launch reports it)
+        work = sc.d_work + 4 * (sc.work_next++ % spt_scene::NWORK);
+        if (hipMemsetAsync(work, 0, 4 * sizeof(int), s) != hipSuccess) return;   // (check_launch reports it)
     }
-    // Heavy tiles (with a learnt order, GEO_WIDE persistent launches): the
-    // first nheavy tiles in dispatch order.  A window of many waves per SIMD
-    // (a full frame: 31.6) runs one heavy tile per SIMD beside lighter
-    // waves; a window of few (a multi-GPU rank's share: N = 8 is 4.0, N = 4
-    // 7.9) is bound by its heaviest tiles' sample chains, so the heaviest 512
-    // (per 256 CUs) walk cooperatively, RT_SPT_COOP_G lanes per pixel
-    // (wide_walk_coop), fetched first by every wave of a block (N = 8) or by
-    // half of them (N = 4).  configs[4], 64 spp (profiles/r03/c4_coop_*.log):
-    // N = 8 windows 18.0-19.8 -> 11.4-14.8 ms, N = 4 18.7 -> 16.9 ms; the
-    // full frame and N = 2 lose with it (28.2 -> 29-31 ms, 21.1 -> 23-24 ms).
-    int nheavy = 0, sp = 0;
+    // Heavy tiles (with a learnt order, GEO_WIDE persistent launches), in
+    // dispatch order: n1 cooperative tiles (RT_SPT_COOP_G lanes per pixel,
+    // wide_walk_coop), fetched first by hw waves of each block, then n2 tiles
+    // routed one per SIMD beside lighter waves, then the rest.  A window of
+    // many waves of work per SIMD (a full frame: 31.6) is throughput-bound:
+    // routing only.  A window of few (a multi-GPU rank's share: N = 8 is 4.0,
+    // N = 4 7.9, N = 2 15.8) is bound by its heaviest tiles' sample chains,
+    // which the cooperative walk shortens ~2x at ~3x their issue cost.
+    // configs[4], 64 spp (profiles/r03/c4_coop_*.log): N = 8 windows
+    // 18.0-19.8 -> 11.4-15.1 ms, N = 4 18.7 -> 17 ms; see DESIGN.md.
+    int n1 = 0, n2 = 0, sp = 0;
     if (GEO == rt::smallpt::GEO_WIDE && RT_WIDE_PERSIST && g.order) {
-        nheavy = std::min(4 * g.nblocks, 4 * g.nslots);
+        n2 = std::min(4 * g.nblocks, 4 * g.nslots);
         const double wps = (double)g.ntiles / (4.0 * sc.cus);
-        if (wps <= 10.0) {
-            nheavy = std::min(2 * sc.cus, 4 * g.nslots);
-            sp = (RT_SPT_COOP_G == 8 ? 3 : 2) | 4 | ((wps <= 5.0 ? 16 : 8) << 3);
+        int hw = 0;
+        if (wps <= 5.0) {
+            n1 = 2 * sc.cus;
+            hw = 16;
+        } else if (wps <= 10.0) {
+            n1 = 2 * sc.cus;
+            hw = 8;
         }
-        if (const char *e = getenv("RT_WIDE_HEAVY")) nheavy = std::min(std::max(atoi(e), 0), 4 * g.nslots);   // A/B
+        if (const char *e = getenv("RT_WIDE_COOP")) n1 = std::max(atoi(e), 0);                  // A/B
+        if (const char *e = getenv("RT_WIDE_HEAVY_WAVES")) hw = std::min(std::max(atoi(e), 0), 16);   // A/B
+        if (n1 > 0) n2 = 0;   // routed tiles beside cooperative ones: N = 4 17 -> 24 ms (c4_coop_tiers_ab.log)
+        if (const char *e = getenv("RT_WIDE_HEAVY")) n2 = std::max(atoi(e), 0);                 // A/B
+        n1 = std::min(n1, 4 * g.nslots);
+        n2 = std::min(n2, 4 * g.nslots - n1);
+        if (n1 > 0) sp = (RT_SPT_COOP_G == 8 ? 3 : 2) | 4 | (hw << 3);
+        if (const char *e = getenv("RT_SPT_SPLIT")) {   // A/B: tier 1 split 2^k ways, a lane per pixel (k < 3)
+            const int k = std::min(std::max(atoi(e), 0), 3);
+            sp = (k == 3 ? (RT_SPT_COOP_G == 8 ? 3 : 2) | 4 : k) | (hw << 3);
+        }
     }
+    const int nheavy = std::min(n1, 0xffff) | (std::min(n2, 0xffff) << 16);
     int split = 0;
     if (GEO == rt::smallpt::GEO_WIDE) {
         int budget = RT_WIDE_BUDGET, batch = RT_BVH_BATCH, stop = RT_WIDE_STOP;
-        // A/B: heavy tiles split 2^k ways (k = 0..2: a lane per pixel), 3: cooperative
-        if (const char *e = getenv("RT_SPT_SPLIT")) {
-            sp = std::min(std::max(atoi(e), 0), 3);
-            if (sp == 3) sp = (RT_SPT_COOP_G == 8 ? 3 : 2) | 4;
-        }
-        if (const char *e = getenv("RT_WIDE_HEAVY_WAVES"))   // A/B: waves per block taking heavy items first
-            sp = (sp & 7) | (std::min(std::max(atoi(e), 0), 16) << 3);
         if (const char *e = getenv("RT_WIDE_OPTS")) sscanf(e, "%d,%d,%d", &budget, &batch, &stop);   // tools: A/B
         split = (RT_WIDE_PERSIST ? sp : 0) | (std::min(std::max(budget, 1), 255) << 8) |
                 (std::min(std::max(batch, 0), 64) << 16) | (std::min(std::max(stop, 0), 64) << 24);
@@ -2224,7 +2241,7 @@ int build_scene_bvh(spt_scene *sc, const rt_sphere *spheres)
     if (e == hipSuccess && wide) e = hipMemcpy(base + w_off, wb.words.data(), w_bytes, hipMemcpyHostToDevice);
     if (e == hipSuccess && wide)
         e = hipMemcpy(base + w_off + w_bytes, wb.maxid.data(), m_bytes, hipMemcpyHostToDevice);
-    if (e == hipSuccess && wide) e = hipMalloc(&sc->d_work, 2 * sizeof(int) * spt_scene::NWORK);
+    if (e == hipSuccess && wide) e = hipMalloc(&sc->d_work, 4 * sizeof(int) * spt_scene::NWORK);
     if (e != hipSuccess) return rtrt::fail_hip(e, "spt_scene_create hierarchy upload");
     rt::smallpt::BvhView &v = sc->bvh;
     v.node = (const float4 *)base;

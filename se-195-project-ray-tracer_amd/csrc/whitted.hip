@@ -424,16 +424,22 @@ struct WfArgs {
     int *ovf;                 // host-mapped flag: set when this frame's pool or a TIR list overflowed
     int pool, fixcap, tcap, ntrees, npix, w;
     int row_begin, row_stride;   // the slab's rows: see slab_row
+    int row_count;               //   (row_count 16-row groups per row_stride)
     int side, nsub;           // sub-sample grid: 3 x 3 (CPU path) or 2 x 2 (openCLcode.cl)
     bool ocl;                 // openCLcode.cl semantics (light colour, refl-first folding, x64)
 };
 
 // Row y of the slab's local row r: slabs interleave in groups of 16 rows (a
-// root block's height), group g of the slab at frame group g*row_stride + k
-// (row_begin = first row + 16k).
+// root block's height).  Local group g of the slab is frame group
+// (g / row_count) * row_stride + g % row_count, counted from row_begin =
+// the first row + 16 x the slab's offset in the period: row_count = 1 for
+// slabs of one group per period (slab k of n: offset k, period n), more for
+// the unequal pair of a two-stream frame (render_async).
 __device__ __forceinline__ int slab_row(const WfArgs &A, int r)
 {
-    return A.row_begin + ((r >> 4) * A.row_stride << 4) + (r & 15);
+    const int g = r >> 4;
+    const int pg = A.row_count == 1 ? g * A.row_stride : (g / A.row_count) * A.row_stride + g % A.row_count;
+    return A.row_begin + (pg << 4) + (r & 15);
 }
 
 // Per-segment item limit of a level based at `base` (the pages left in the pool).
@@ -930,6 +936,10 @@ constexpr int SLOT_WF2 = 9;
 // frame's mix of sphere / plane / background rows and so its queue fill.
 constexpr long long SLAB_TREES = 18000000;
 constexpr long long STREAM2_TREES = 4000000;   // frames from this size on: two slabs on two streams
+#ifndef WF_SPLIT_P
+#define WF_SPLIT_P 1                            // row groups of the first / second of those slabs per period
+#define WF_SPLIT_Q 1
+#endif
 // Record pool (levels 1..5 together) as a fraction of the slab's trees, to
 // start with.  The reference scene needs 0.83 at 1080p (14.2 M nodes for
 // 17.1 M trees) but 0.94 at 640 x 480 (its rows [20, 410) hold more of the
@@ -1120,7 +1130,27 @@ int render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int 
         nslab = std::min<long long>(std::max<long long>(nslab, 2), ngroups);
         if (nslab < 2) nstream = 1;
     }
-    const int slab_rows = (int)((ngroups + nslab - 1) / nslab) * 16;
+    // Two slabs on two streams: the second slab's root kernel can start only
+    // once the first's root grid is dispatched (~0.37 ms in at 1080p), so
+    // with equal slabs the second ends ~0.16 ms after the first
+    // (profiles/r03/whitted_two_stream_timeline.txt).  The first takes p of
+    // every p + q row groups (RT_WHITTED_SPLIT=p,q; 1,1: equal).
+    int sp_p = 1, sp_q = 1;
+    if (nstream == 2 && nslab == 2) {
+        sp_p = WF_SPLIT_P;
+        sp_q = WF_SPLIT_Q;
+        if (const char *e = getenv("RT_WHITTED_SPLIT")) sscanf(e, "%d,%d", &sp_p, &sp_q);   // A/B
+        sp_p = std::min(std::max(sp_p, 1), 64);
+        sp_q = std::min(std::max(sp_q, 1), 64);
+    }
+    const int period = sp_p + sp_q;
+    const auto split_groups = [&](int k) {      // 16-row groups of slab k of an unequal pair
+        const int full = ngroups / period, rem = ngroups % period;
+        return k == 0 ? full * sp_p + std::min(rem, sp_p) : full * sp_q + std::max(0, std::min(rem - sp_p, sp_q));
+    };
+    const bool unequal = nstream == 2 && nslab == 2 && !(sp_p == 1 && sp_q == 1);
+    const int slab_rows = unequal ? std::max(split_groups(0), split_groups(1)) * 16
+                                  : (int)((ngroups + nslab - 1) / nslab) * 16;
     rt::whitted::WfArgs A[2];
     hipStream_t ss[2] = {s, s};
     if (nstream == 2) {
@@ -1136,15 +1166,17 @@ int render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int 
         A[i].side = side;
         A[i].nsub = nsub;
         A[i].ocl = ocl;
-        A[i].row_stride = (int)nslab;
+        A[i].row_stride = unequal ? period : (int)nslab;
+        A[i].row_count = unequal ? (i == 0 ? sp_p : sp_q) : 1;
         hipLaunchKernelGGL(rt::whitted::scene_kernel, dim3(1), dim3(64), 0, ss[i], d_prims, nprims,
                            (rt::whitted::Scene *)A[i].scene);
     }
     for (int k = 0; k < (int)nslab; k++) {
         rt::whitted::WfArgs &a = A[k % nstream];
         hipStream_t sk = ss[k % nstream];
-        const int srows = (int)((ngroups - k + nslab - 1) / nslab) * 16;
-        a.row_begin = row_begin + 16 * k;
+        const int srows = unequal ? split_groups(k) * 16 : (int)((ngroups - k + nslab - 1) / nslab) * 16;
+        if (srows == 0) continue;                // (an unequal pair over fewer groups than its period)
+        a.row_begin = row_begin + 16 * (unequal && k == 1 ? sp_p : k);
         a.npix = w * srows;
         a.ntrees = a.npix * nsub;
         hipError_t e = hipMemsetAsync(a.count, 0, sizeof(int) * rt::whitted::C_TOTAL * rt::whitted::CSTRIDE, sk);

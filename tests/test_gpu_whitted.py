@@ -134,6 +134,19 @@ def test_interleaved_slabs_bit_exact(rt, oracle, slabs, monkeypatch):
     assert (got == ref).all() and gc == rc
 
 
+@pytest.mark.parametrize("split", ["5,3", "2,1", "1,3", "7,6"])
+def test_unequal_two_stream_slabs_bit_exact(rt, oracle, split, monkeypatch):
+    """Two slabs on two streams that take unequal shares of the 16-row groups
+    (RT_WHITTED_SPLIT=p,q: the first slab p of every p + q groups, the
+    second q) give the same frame and counts, at a ragged height too."""
+    monkeypatch.setenv("RT_WHITTED_STREAMS", "2")
+    monkeypatch.setenv("RT_WHITTED_SPLIT", split)
+    for w, h in ((320, 240), (200, 170)):
+        ref, rc = oracle.whitted_render(w, h, nthreads=8)
+        got, gc = rt.whitted_render(w, h, counters=True)
+        assert (got == ref).all() and gc == rc
+
+
 def test_device_memory_bounded(rt):
     """The level pass's device arena for a 1920x1080 frame (two slabs of
     queues at a third of the slab's trees per level) stays near 1.2 GB."""

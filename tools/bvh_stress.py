@@ -6,7 +6,7 @@ rendered with the hierarchy and with the full scan (RT_SPT_NO_BVH) and
 compared bit for bit (colours, seeds, pixels, work counters).
 
     N=60 python tools/bvh_stress.py
-    REPEAT=3 RT_SPT_SPLIT=3 N=60 python tools/bvh_stress.py   # learnt order: cooperative heavy tiles
+    REPEAT=3 N=60 python tools/bvh_stress.py   # learnt order: cooperative heavy tiles (small frames)
 """
 import os
 import sys
