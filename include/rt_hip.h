@@ -89,6 +89,13 @@ int rt_set_device(int device);
 int rt_release(void);
 /* Bytes of device memory the blocking entry points currently cache. */
 size_t rt_cached_bytes(void);
+/* Page-locked host memory (hipHostMalloc) for frames the host reads back
+ * every pass -- the smallpt drop-in's `pixels` (smallptGPU.cpp:111, a plain
+ * malloc there, read by ReadKernelBuffer :626 after every pass): its
+ * device-to-host copy then runs at DMA speed instead of through a staging
+ * buffer.  rt_host_free(NULL) is a no-op. */
+int rt_host_alloc(size_t bytes, void **out);
+int rt_host_free(void *p);
 
 /* ------------------------------------------------------------ Whitted */
 /* Blocking, host buffers.  Renders rows [row_begin,row_end) of the w x h

@@ -245,6 +245,23 @@ extern "C" size_t rt_cached_bytes(void)
     return s;
 }
 
+extern "C" int rt_host_alloc(size_t bytes, void **out)
+{
+    if (!out || bytes == 0) return rtrt::fail(RT_ERR_INVALID, "rt_host_alloc: bad arguments");
+    *out = nullptr;
+    hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rt_host_alloc");
+    return RT_OK;
+}
+
+extern "C" int rt_host_free(void *p)
+{
+    if (!p) return RT_OK;
+    hipError_t e = hipHostFree(p);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "rt_host_free");
+    return RT_OK;
+}
+
 extern "C" void spt_seed_fill(uint32_t *seeds, size_t n, unsigned seed)
 {
     srand(seed);

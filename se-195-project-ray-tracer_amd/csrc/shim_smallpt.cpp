@@ -90,7 +90,7 @@ void FreeBuffers()
     if (frame) spt_multi_destroy(frame);
     frame = nullptr;
     free(h_seeds);
-    free(pixels);
+    (void)rt_host_free(pixels);
     h_seeds = nullptr;
     pixels = nullptr;
 }
@@ -106,7 +106,12 @@ void AllocateBuffers()
         h_seeds[i] = (uint32_t)rand();
         if (h_seeds[i] < 2) h_seeds[i] = 2;
     }
-    pixels = (unsigned int *)malloc(sizeof(unsigned int) * pixelCount);
+    // page-locked: the blocking read after every pass (ReadKernelBuffer)
+    // then runs at DMA speed
+    void *px = nullptr;
+    int rc0 = rt_host_alloc(sizeof(unsigned int) * pixelCount, &px);
+    if (rc0) die("Failed to allocate the pixel buffer", rc0);
+    pixels = (unsigned int *)px;
     for (int i = 0; i < pixelCount; ++i) pixels[i] = i;
     int rc = spt_multi_create(spheres, sphereCount, width, height, devices.data(), (int)devices.size(), &frame);
     if (rc) die("Failed to create HIP buffers", rc);
@@ -184,7 +189,9 @@ void UpdateRenderingGPU()
     if (rc) die("Failed to read the HIP pixel buffer", rc);
     const double elapsedTime = WallClockTime() - startTime;
     const int samples = currentSample - startSampleCount;
-    const double sampleSec = samples * height * width / elapsedTime;
+    // (in double: the reference's int product overflows past ~1,000 samples
+    // per call at 1080p, which its OpenCL device never reached in one call)
+    const double sampleSec = (double)samples * height * width / elapsedTime;
     sprintf(captionBuffer, "Rendering time %.3f sec (pass %d)  Sample/sec  %.1fK\n", elapsedTime,
             currentSample, sampleSec / 1000.f);
 }

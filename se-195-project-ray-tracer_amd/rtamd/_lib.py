@@ -16,6 +16,7 @@ SPT_PATH_TRACING, SPT_DIRECT_LIGHTING = 0, 1
 
 # Every symbol include/rt_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = ("rt_last_error", "rt_device_count", "rt_set_device", "rt_release", "rt_cached_bytes",
+           "rt_host_alloc", "rt_host_free",
            "rtw_render", "rtw_render_async", "rtw_render_ocl", "rtw_render_ocl_async", "spt_render", "spt_render_async", "spt_seed_fill",
            "spt_scene_create", "spt_scene_destroy", "spt_scene_render_async", "spt_scene_render_groups_async",
            "spt_pack_pixels_async",
@@ -87,6 +88,8 @@ def lib():
     L.rt_device_count.restype = i
     L.rt_set_device.argtypes = [i]
     L.rt_cached_bytes.restype = C.c_size_t
+    L.rt_host_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p)]
+    L.rt_host_free.argtypes = [C.c_void_p]
     L.rtw_render.argtypes = [vp, i, vp, i, i, i, i, u64p]
     L.rtw_render_async.argtypes = [vp, i, vp, i, i, i, i, u64p, vp]
     L.rtw_render_ocl.argtypes = [vp, i, vp, i, i, u64p]
