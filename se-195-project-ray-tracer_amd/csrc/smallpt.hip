@@ -849,23 +849,27 @@ __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigne
 // the highest reference index on ties, an order-independent choice.
 // G = 4 (COOP4): four lanes per pixel, two child slots / spheres per lane --
 // half the waves per heavy tile for a somewhat longer trip.
-__device__ __forceinline__ int dpp_xor1(int v) { return __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false); }
-__device__ __forceinline__ int dpp_xor2(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false); }
-__device__ __forceinline__ int dpp_mir8(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false); }
+// Minimum over the group of non-negative floats (leaf distances: > EPS or
+// +inf), compared as integers: the same order, and no NaN canonicalisation.
 template <int G>
 __device__ __forceinline__ float grp_min(float v)
 {
-    v = fminf(v, __int_as_float(dpp_xor1(__float_as_int(v))));
-    v = fminf(v, __int_as_float(dpp_xor2(__float_as_int(v))));
-    if (G == 8) v = fminf(v, __int_as_float(dpp_mir8(__float_as_int(v))));
-    return v;
+    // (the identity as the DPP's old value lets the compiler fold each move
+    // into its v_min_i32)
+    constexpr int ID = 0x7fffffff;
+    int i = __float_as_int(v);
+    i = min(i, __builtin_amdgcn_update_dpp(ID, i, 0xB1, 0xF, 0xF, false));
+    i = min(i, __builtin_amdgcn_update_dpp(ID, i, 0x4E, 0xF, 0xF, false));
+    if (G == 8) i = min(i, __builtin_amdgcn_update_dpp(ID, i, 0x141, 0xF, 0xF, false));
+    return __int_as_float(i);
 }
 template <int G>
 __device__ __forceinline__ int grp_max(int v)
 {
-    v = max(v, dpp_xor1(v));
-    v = max(v, dpp_xor2(v));
-    if (G == 8) v = max(v, dpp_mir8(v));
+    constexpr int ID = (int)0x80000000;
+    v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0xB1, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0x4E, 0xF, 0xF, false));
+    if (G == 8) v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0x141, 0xF, 0xF, false));
     return v;
 }
 // The group's G bits of a predicate (bit k = lane gbase + k).
