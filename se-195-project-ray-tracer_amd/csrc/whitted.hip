@@ -362,8 +362,9 @@ __device__ __forceinline__ void load_scene(Scene &S, const Scene *__restrict__ g
 //                  level L-1 appended (wave-aggregated atomics);
 //   tir_kernel     after level L: the refraction children of its TIR nodes
 //                  (see below), appended to level L+1;
-//   backacc_kernel levels 4..1: node colour += refraction child (Beer factor)
-//                  then += reflection child (:476-511), children final first;
+//   backacc_kernel node colour += refraction child (Beer factor) then +=
+//                  reflection child (:476-511), children final first: levels
+//                  3 and 1, each folding the two levels below it in registers;
 //   final_kernel   level 0 of the nine trees of a pixel + the sum / x28 pack.
 // Records hold what back-accumulation needs (colour, distance, primitive, TIR)
 // and the queue slots of the node's two children.
@@ -693,29 +694,28 @@ tir_kernel(WfArgs A, int L, const float *__restrict__ sx_tab, const float *__res
 
 // Back-accumulation of one node (raytracer.cpp:476-511): the refraction child
 // (Beer factor from the node's own distance and colour, unless TIR) first,
-// then the reflection child (colour x refl).
-__device__ __forceinline__ float4 accumulate(const Scene &S, float4 pc, int pinfo, int2 ch,
-                                             const float4 *__restrict__ ccol, bool ocl)
+// then the reflection child (colour x refl).  cx / cy: the children's final
+// colours (read only where ch.x / ch.y >= 0).
+__device__ __forceinline__ float4 accumulate(const Scene &S, float4 pc, int pinfo, int2 ch, float4 cx, float4 cy,
+                                             bool ocl)
 {
     const float4 pm = S.mat0[pinfo & 0xff];
     const auto refr = [&]() {
         if (ch.y < 0) return;
-        const float4 cc = ccol[ch.y];
-        float ax = cc.x, ay = cc.y, az = cc.z;
+        float ax = cy.x, ay = cy.y, az = cy.z;
         if (!(pinfo & INFO_TIR)) {
             const float nd = -pc.w;
-            ax = cc.x * rtm::expf(pm.x * 0.15f * nd);
-            ay = cc.y * rtm::expf(pm.y * 0.15f * nd);
-            az = cc.z * rtm::expf(pm.z * 0.15f * nd);
+            ax = cy.x * rtm::expf(pm.x * 0.15f * nd);
+            ay = cy.y * rtm::expf(pm.y * 0.15f * nd);
+            az = cy.z * rtm::expf(pm.z * 0.15f * nd);
         }
         pc.x += ax; pc.y += ay; pc.z += az;
     };
     const auto refl = [&]() {
         if (ch.x < 0) return;
-        const float4 cc = ccol[ch.x];
-        pc.x += cc.x * pm.x * pm.w;
-        pc.y += cc.y * pm.y * pm.w;
-        pc.z += cc.z * pm.z * pm.w;
+        pc.x += cx.x * pm.x * pm.w;
+        pc.y += cx.y * pm.y * pm.w;
+        pc.z += cx.z * pm.z * pm.w;
     };
     if (ocl) {                     // openCLcode.cl:199-233: reflection child first
         refl();
@@ -727,6 +727,33 @@ __device__ __forceinline__ float4 accumulate(const Scene &S, float4 pc, int pinf
     return pc;
 }
 
+// Final colour of pool node c, whose descendants D levels down are final:
+// the D levels between are folded in registers, bottom-up per child, and
+// never written back (nothing but their parent reads them).  D = 0: the
+// node's colour as stored.  A level-5 node (no lchild record) is only ever
+// reached with D = 0.
+template <int D>
+__device__ __forceinline__ float4 folded(const WfArgs &A, const Scene &S, int c)
+{
+    float4 cc = A.lcol[c];
+    if constexpr (D > 0) {
+        const int2 g = A.lchild[c];
+        if (g.x >= 0 || g.y >= 0) {
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 cx = g.x >= 0 ? folded<D - 1>(A, S, g.x) : z;
+            const float4 cy = g.y >= 0 ? folded<D - 1>(A, S, g.y) : z;
+            cc = accumulate(S, cc, A.linfo[c], g, cx, cy, A.ocl);
+        }
+    }
+    return cc;
+}
+
+// Back-accumulation of level L's nodes with their D levels below
+// (folded<D>), written back: D = 1 is a launch per level (4, 3, 2, 1); D = 2
+// folds levels (3 <- 4 <- 5) and (1 <- 2 <- 3) in two launches, the default
+// (WF_BACKACC_LEVELS).  Levels written: only those a later launch or
+// final_kernel reads as final.
+template <int D>
 __global__ void __launch_bounds__(256)
 backacc_kernel(WfArgs A, int L)
 {
@@ -740,12 +767,17 @@ backacc_kernel(WfArgs A, int L)
         if (lane >= nvalid) continue;
         const int2 ch = A.lchild[q];
         if (ch.x < 0 && ch.y < 0) continue;
-        A.lcol[q] = accumulate(S, A.lcol[q], A.linfo[q], ch, A.lcol, A.ocl);
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 cx = ch.x >= 0 ? folded<D - 1>(A, S, ch.x) : z;
+        const float4 cy = ch.y >= 0 ? folded<D - 1>(A, S, ch.y) : z;
+        A.lcol[q] = accumulate(S, A.lcol[q], A.linfo[q], ch, cx, cy, A.ocl);
     }
 }
 
-// Level 0 of the pixel's nine trees, the sum over sub-samples (:513-515) and
-// the x28 / clamp / XRGB pack (:517-523).
+// Level 0 of the pixel's nine trees, folded with the FD levels below it
+// (level FD's colours final), the sum over sub-samples (:513-515) and the
+// x28 / clamp / XRGB pack (:517-523).
+template <int FD>
 __global__ void __launch_bounds__(256)
 final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
 {
@@ -764,7 +796,12 @@ final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
         float4 c0 = A.rcol[tree];
         if (!flagged(A, tree)) {
             const int2 ch = A.rchild[tree];
-            if (ch.x >= 0 || ch.y >= 0) c0 = accumulate(S, c0, A.rinfo[tree], ch, A.lcol, A.ocl);
+            if (ch.x >= 0 || ch.y >= 0) {
+                const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 cx = ch.x >= 0 ? folded<FD - 1>(A, S, ch.x) : z;
+                const float4 cy = ch.y >= 0 ? folded<FD - 1>(A, S, ch.y) : z;
+                c0 = accumulate(S, c0, A.rinfo[tree], ch, cx, cy, A.ocl);
+            }
         }
         tr += c0.x; tg += c0.y; tb += c0.z;
     }
@@ -940,6 +977,9 @@ constexpr long long STREAM2_TREES = 4000000;   // frames from this size on: two 
 #define WF_SPLIT_P 1                            // row groups of the first / second of those slabs per period
 #define WF_SPLIT_Q 1
 #endif
+#ifndef WF_BACKACC_LEVELS
+#define WF_BACKACC_LEVELS 2                     // levels folded per back-accumulation launch (1 or 2)
+#endif
 // Record pool (levels 1..5 together) as a fraction of the slab's trees, to
 // start with.  The reference scene needs 0.83 at 1080p (14.2 M nodes for
 // 17.1 M trees) but 0.94 at 640 x 480 (its rows [20, 410) hold more of the
@@ -1089,9 +1129,31 @@ int launch_wavefront(const rt::whitted::WfArgs &A, int w, int rows, int row_end,
         hipLaunchKernelGGL(level_kernel<COUNT>, dim3(level_blocks), block, 0, s, A, L, cnt);
     }
     hipLaunchKernelGGL(fixup_kernel<COUNT>, dim3(256), dim3(64), 0, s, A, d_sx, d_sy, DX, DY, cnt);
-    for (int L = LEVELS - 2; L >= 1; L--)
-        hipLaunchKernelGGL(backacc_kernel, dim3(qblocks), block, 0, s, A, L);
-    hipLaunchKernelGGL(final_kernel, tiles, block, 0, s, A, row_end, d_xrgb);
+    // Back-accumulation schedule (RT_WHITTED_BACKACC, A/B): 1 = a launch per
+    // level 4..1; 2 = levels (3 <- 4 <- 5), (1 <- 2 <- 3); 3 = (2 <- 3 <- 4 <- 5)
+    // and the final kernel folds 0 <- 1 <- 2; 4 = (3 <- 4 <- 5) and the final
+    // kernel folds 0 <- 1 <- 2 <- 3.
+    static const int backacc = [] {
+        const char *e = getenv("RT_WHITTED_BACKACC");
+        const int v = e ? atoi(e) : WF_BACKACC_LEVELS;
+        return v >= 1 && v <= 4 ? v : WF_BACKACC_LEVELS;
+    }();
+    static_assert(LEVELS == 6, "the back-accumulation schedules assume levels 0..5");
+    if (backacc == 1) {
+        for (int L = LEVELS - 2; L >= 1; L--)
+            hipLaunchKernelGGL(backacc_kernel<1>, dim3(qblocks), block, 0, s, A, L);
+        hipLaunchKernelGGL(final_kernel<1>, tiles, block, 0, s, A, row_end, d_xrgb);
+    } else if (backacc == 2) {
+        hipLaunchKernelGGL(backacc_kernel<2>, dim3(qblocks), block, 0, s, A, 3);
+        hipLaunchKernelGGL(backacc_kernel<2>, dim3(qblocks), block, 0, s, A, 1);
+        hipLaunchKernelGGL(final_kernel<1>, tiles, block, 0, s, A, row_end, d_xrgb);
+    } else if (backacc == 3) {
+        hipLaunchKernelGGL(backacc_kernel<3>, dim3(qblocks), block, 0, s, A, 2);
+        hipLaunchKernelGGL(final_kernel<2>, tiles, block, 0, s, A, row_end, d_xrgb);
+    } else {
+        hipLaunchKernelGGL(backacc_kernel<2>, dim3(qblocks), block, 0, s, A, 3);
+        hipLaunchKernelGGL(final_kernel<3>, tiles, block, 0, s, A, row_end, d_xrgb);
+    }
     return rtrt::check_launch("rtw wavefront kernels");
 }
 
