@@ -387,7 +387,8 @@ __device__ __forceinline__ void load_scene(Scene &S, const Scene *__restrict__ g
 constexpr int LEVELS = 6;
 constexpr int INFO_TIR = 0x100;       // refr > 0 but no refraction ray (TIR)
 constexpr int INFO_REFR_OK = 0x200;   // the node wrote a refraction ray
-constexpr int NODE_SHIFT = 16;        // linfo bits 16..21: the node's index (0..62)
+constexpr int TREE_BITS = 25;         // queued item: tree | node << TREE_BITS (node 0..62; < 2^25 trees a slab)
+constexpr int TREE_MASK = (1 << TREE_BITS) - 1;
 using lq::NSEG;
 using lq::PAGE;
 using lq::PAGE_ROW;
@@ -416,9 +417,9 @@ struct WfArgs {
     int *fixlist;             // [fixcap] flagged trees (fixup scans fixbits when more)
     // The record pool (levels 1..5), indexed by pool slot.
     float4 *ia;               // queued ray: o.xyz, d.x
-    float4 *ib;               // d.y, d.z, rindex, tree (int bits)
+    float4 *ib;               // d.y, d.z, rindex, tree | node << TREE_BITS (int bits)
     float4 *lcol;             // node colour.xyz, dist
-    int *linfo;               // node << NODE_SHIFT (queued), then | hit primitive | INFO_* (traced)
+    int *linfo;               // traced node: hit primitive | INFO_*
     int2 *lchild;             // pool slots of the node's children
     int4 *tir[LEVELS];        // [tcap] TIR nodes of level L (0..4): slot, tree, node, rindex (bits)
     int *count;               // [C_TOTAL * CSTRIDE]
@@ -471,8 +472,10 @@ __device__ __forceinline__ void put_item(const WfArgs &A, int L, int slot, const
                                          int node)
 {
     A.ia[slot] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-    A.ib[slot] = make_float4(r.d.y, r.d.z, rin, __int_as_float(tree));
-    if (L < LEVELS - 1) A.linfo[slot] = node << NODE_SHIFT;   // level 5 needs no node index
+    // The node index rides in the item's tree word (no separate 4-B write here
+    // and read at trace time: 8 B per queued node).
+    (void)L;
+    A.ib[slot] = make_float4(r.d.y, r.d.z, rin, __int_as_float(tree | (node << TREE_BITS)));
 }
 
 // Queues the children of node `node` (level L < 5, record `slot_self`) into
@@ -606,11 +609,11 @@ level_kernel(WfArgs A, int L, unsigned long long *__restrict__ counters)
         int tree = 0, node = 0;
         if (active) {
             const float4 a = A.ia[q], b = A.ib[q];
-            node = L < LEVELS - 1 ? A.linfo[q] >> NODE_SHIFT : 0;
             ray3 r;
             r.o = mk(a.x, a.y, a.z);
             r.d = mk(a.w, b.x, b.y);
-            tree = __float_as_int(b.w);
+            tree = __float_as_int(b.w) & TREE_MASK;
+            node = __float_as_int(b.w) >> TREE_BITS;
             hh = trace<COUNT>(S, r, b.z, cnt, A.ocl);
             tir = hh.refr > 0 && !hh.refr_ray_ok;
             if (tir && L < 5) cnt.tir++;                // node index < 31 (:398)
@@ -1057,7 +1060,7 @@ int wavefront_arena(rtrt::DeviceState &st, int slot, int w, int rows, int nsub, 
 {
     using namespace rt::whitted;
     const size_t T = (size_t)w * rows * nsub;
-    if (T > (size_t)0x7fffffff / 2) return rtrt::fail(RT_ERR_INVALID, "rtw: frame too large");
+    if (T > (size_t)TREE_MASK + 1) return rtrt::fail(RT_ERR_INVALID, "rtw: slab too large");   // item tree word
     // RT_WHITTED_QUEUE_CAP lowers the pool (test hook: exercises the
     // overflow -> fixup path).
     int *ovf = nullptr;
@@ -1179,6 +1182,10 @@ int render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int 
     const int ngroups = (rows + 15) / 16;                // 16-row groups (slab_row)
     long long nslab = ((long long)w * ngroups * 16 * nsub + SLAB_TREES - 1) / SLAB_TREES;
     if (const char *e = getenv("RT_WHITTED_SLABS")) nslab = std::max(1, atoi(e));   // test hook
+    {   // at most 2^TREE_BITS trees a slab (the queued items' tree word)
+        const long long max_groups = std::max<long long>(1, ((long long)rt::whitted::TREE_MASK + 1) / ((long long)w * 16 * nsub));
+        nslab = std::max<long long>(nslab, (ngroups + max_groups - 1) / max_groups);
+    }
     nslab = std::min<long long>(std::max<long long>(nslab, 1), ngroups);
     // Frames of >= 4 M trees run as (at least) two slabs that alternate
     // between the caller's stream and a second one, each with its own arena:
