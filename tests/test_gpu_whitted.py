@@ -147,6 +147,18 @@ def test_unequal_two_stream_slabs_bit_exact(rt, oracle, split, monkeypatch):
         assert (got == ref).all() and gc == rc
 
 
+def test_slab_tree_word_limit(rt, monkeypatch):
+    """A queued item carries tree | node << 25, so a slab holds at most 2^25
+    trees: a 3840x2400 frame (~80 M trees) forced into one slab
+    (RT_WHITTED_SLABS=1) is split into enough slabs by the library and
+    renders the same frame and counts as the default slab plan."""
+    w, h = 3840, 2400
+    ref, rc = rt.whitted_render(w, h, counters=True)
+    monkeypatch.setenv("RT_WHITTED_SLABS", "1")
+    got, gc = rt.whitted_render(w, h, counters=True)
+    assert (got == ref).all() and gc == rc
+
+
 def test_device_memory_bounded(rt):
     """The level pass's device arena for a 1920x1080 frame (two slabs of
     queues at a third of the slab's trees per level) stays near 1.2 GB."""
