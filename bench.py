@@ -307,15 +307,23 @@ def c5_line(args, dev):
     s = torch.cuda.current_stream(dev)
     L = rtamd.lib()
 
-    def run(c):
+    def run(c, mode=rtamd.SPT_PATH_TRACING):
         rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
                                              seeds.data_ptr(), px.data_ptr(), W, H, 0, H, 0, SPP,
-                                             rtamd.SPT_PATH_TRACING, c.data_ptr() if c is not None else None,
-                                             s.cuda_stream))
+                                             mode, c.data_ptr() if c is not None else None, s.cuda_stream))
 
+    # Rays (Intersect + IntersectP calls) from a rays-only counted frame
+    # (SPT_COUNT_RAYS: the uncounted walks); the reference's sphere-test count
+    # from a full-counter frame (its shadow queries must find IntersectP's
+    # early-exit position, the highest-index occluder).
+    run(cnt, rtamd.SPT_PATH_TRACING | rtamd.SPT_COUNT_RAYS)
+    torch.cuda.synchronize(dev)
+    rays_counts = cnt.tolist()
+    cnt.zero_()
     run(cnt)
     torch.cuda.synchronize(dev)
     counts = cnt.tolist()
+    assert rays_counts[0] == counts[0] and rays_counts[1] == counts[1], (rays_counts, counts)
     # Steady state, as the headline steps: the first launches of a (window,
     # camera, spp) key record the tile groups' costs and build the
     # heaviest-first order (SptSched); then the median of three frames.
@@ -424,14 +432,14 @@ def dropin_line(args):
     return out
 
 
-def tiled_line(step, cnt, dev, world, distributed, workload, spp, frames=2, warm=0, **scene):
+def tiled_line(step, cnt, dev, world, distributed, workload, spp, frames=2, warm=0, mode=0, **scene):
     """A frame of `workload` tiled across the job's GPUs exactly as the
     headline steps are (each rank renders its rows, then the RCCL all-gather
     + repack): a counted frame, `warm` untimed frames (hierarchy scenes learn
     their heaviest-first order over a key's first launches), then `frames`
     timed frames bracketed by barrier + synchronize, max over ranks."""
     cnt.zero_()
-    step(counters=cnt, spp=spp, **scene)
+    step(counters=cnt, spp=spp, cmode=mode, **scene)
     for _ in range(warm):
         step(spp=spp, **scene)
     torch.cuda.synchronize(dev)
@@ -461,6 +469,132 @@ def tiled_line(step, cnt, dev, world, distributed, workload, spp, frames=2, warm
             "Msamples_per_s": round(W * H * spp / ms / 1e3, 2), "rays_per_frame": rays}
 
 
+def list_tiled_line(dev, rank, world, distributed, s, sc, cm, spp, workload, frames=3, warm=2):
+    """BASELINE configs[4] at N > 1 split by measured cost: one learning frame
+    renders the interleaved shares as tile-group lists recording every
+    group's wave time (spt_scene_render_list_async), the costs are summed over
+    the ranks (all-reduce), and every rank takes its list from the same
+    deterministic longest-first partition (rtamd.dist.balanced_partition:
+    each rank gets an equal share of the heaviest groups and of the total).
+    Timed frames: render the list, then the group exchange (pack, one
+    all-gather, unpack) and the RGBA8 repack on a second stream, overlapped
+    with the next frame's render (double-buffered); barrier + synchronize
+    around them, max over ranks."""
+    L = rtamd.lib()
+    ng = rdist.group_count(W, H)
+    seeds0 = torch.from_numpy(rtamd.scenes.seeds(W, H).view(np.int32)).to(dev)
+    seeds = torch.empty_like(seeds0)
+    cols = [torch.zeros(3 * W * H, dtype=torch.float32, device=dev) for _ in range(2)]
+    pxs = [torch.zeros(W * H, dtype=torch.int32, device=dev) for _ in range(2)]
+    cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+    cost = torch.zeros(ng, dtype=torch.int32, device=dev)
+
+    def render(lst, b, counters=None, cost_buf=None):
+        rtamd.check(L.spt_scene_render_list_async(
+            sc.handle, C.byref(cm), cols[b].data_ptr(), seeds0.data_ptr(), seeds.data_ptr(), pxs[b].data_ptr(),
+            W, H, lst.data_ptr(), lst.numel(), 0, spp, rtamd.SPT_PATH_TRACING | rtamd.SPT_COUNT_RAYS,
+            counters.data_ptr() if counters is not None else None,
+            cost_buf.data_ptr() if cost_buf is not None else None, s.cuda_stream))
+
+    mine0 = torch.tensor(rdist.interleaved_groups(rank, world, W, H), dtype=torch.int32, device=dev)
+    render(mine0, 0, counters=cnt, cost_buf=cost)            # learning frame: costs + rays (rays-only mode)
+    torch.cuda.synchronize(dev)
+    costs = cost.to(torch.int64)
+    counts = cnt.clone()
+    if distributed:
+        dist.all_reduce(costs)
+        dist.all_reduce(counts)
+    costs = costs.cpu().numpy()
+    counts = counts.tolist()
+    parts = rdist.balanced_partition(costs, world)
+    mine = torch.tensor(parts[rank], dtype=torch.int32, device=dev)
+    gs = torch.cuda.Stream(dev)
+
+    def pack_groups(c, groups, n, buf):
+        rtamd.check(L.spt_groups_pack_async(c.data_ptr(), W, H, groups.data_ptr(), n, buf.data_ptr(),
+                                            torch.cuda.current_stream(dev).cuda_stream))
+
+    def unpack_groups(c, groups, n, buf):
+        rtamd.check(L.spt_groups_unpack_async(c.data_ptr(), W, H, groups.data_ptr(), n, buf.data_ptr(),
+                                              torch.cuda.current_stream(dev).cuda_stream))
+
+    def packer(b):
+        return lambda: rtamd.check(L.spt_pack_pixels_async(cols[b].data_ptr(), pxs[b].data_ptr(), W, H, 0, H,
+                                                           torch.cuda.current_stream(dev).cuda_stream))
+
+    gathers = [rdist.ListGather(cols[b], pxs[b], rank, world, W, H, parts, pack=packer(b), pack_groups=pack_groups,
+                                unpack_groups=unpack_groups) for b in range(2)]
+    freed = [None, None]
+    rev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(frames)]
+    nf = [0]
+
+    def frame(i=None):
+        b = nf[0] % 2
+        nf[0] += 1
+        if freed[b] is not None:
+            s.wait_event(freed[b])
+        if i is not None:
+            rev[i][0].record(s)
+        render(mine, b)
+        if i is not None:
+            rev[i][1].record(s)
+        if world > 1:
+            gs.wait_stream(s)
+            with torch.cuda.stream(gs):
+                gathers[b].gather()
+            freed[b] = torch.cuda.Event()
+            freed[b].record(gs)
+        return b
+
+    for _ in range(warm):
+        frame()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    last = 0
+    for i in range(frames):
+        last = frame(i)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    render_ms = float(np.median([a.elapsed_time(b) for a, b in rev]))
+    per_rank = [render_ms]
+    if distributed:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+        mine_t = torch.tensor([render_ms], dtype=torch.float64, device=dev)
+        allr = [torch.zeros_like(mine_t) for _ in range(world)]
+        dist.all_gather(allr, mine_t)
+        per_rank = [round(x.item(), 3) for x in allr]
+    ms = el * 1e3 / frames
+    rays = counts[0] + counts[1]
+    out = {"workload": "%s, cost-balanced tile-group lists over %d GPU(s) + %s group all-gather" % (
+               workload, world, collective_name()),
+           "n_gpus": world, "ms_per_frame": round(ms, 3), "Mrays_per_s": round(rays / ms / 1e3, 2),
+           "Msamples_per_s": round(W * H * spp / ms / 1e3, 2), "rays_per_frame": rays,
+           "partition": "rtamd.dist.balanced_partition over one learning frame's per-group wave times",
+           "render_ms_per_rank": per_rank,
+           "predicted_load_per_rank": [int(costs[p].sum()) for p in parts]}
+    # the assembled frame must equal one GPU rendering the whole frame
+    ref_c = torch.zeros_like(cols[0])
+    ref_p = torch.zeros_like(pxs[0])
+    ref_s = torch.empty_like(seeds0)
+    rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cm), ref_c.data_ptr(), seeds0.data_ptr(),
+                                         ref_s.data_ptr(), ref_p.data_ptr(), W, H, 0, H, 0, spp,
+                                         rtamd.SPT_PATH_TRACING, None, s.cuda_stream))
+    torch.cuda.synchronize(dev)
+    ok = torch.tensor([int(torch.equal(ref_c.view(torch.int32), cols[last].view(torch.int32))
+                           and torch.equal(ref_p, pxs[last]))], dtype=torch.int32, device=dev)
+    if distributed:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    out["frame_check"] = "assembled frame == single-GPU frame (bit-exact)" if ok.item() else "MISMATCH"
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -476,10 +610,26 @@ def main():
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(gpu)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group(backend)
+        # Fail fast, with the collective library's own message, if the
+        # communicator cannot be built or used: a short timeout and one tiny
+        # all-reduce right after init (an RCCL failure otherwise surfaces
+        # minutes later as a hang in the first frame's gather).
+        import datetime
+        try:
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", gpu),
+                                        timeout=datetime.timedelta(seconds=180))
+            else:
+                dist.init_process_group(backend, timeout=datetime.timedelta(seconds=180))
+            probe = torch.ones(1, device=torch.device("cuda", gpu))
+            dist.all_reduce(probe)
+            torch.cuda.synchronize(gpu)
+            if int(probe.item()) != world:
+                raise RuntimeError("all-reduce probe returned %r, expected %d" % (probe.item(), world))
+        except Exception as e:      # noqa: BLE001 -- reported verbatim, then exit non-zero
+            print(json.dumps({"error": "collective init failed on rank %d (%s backend): %s: %s" % (
+                rank, collective_name(), type(e).__name__, e)}), flush=True)
+            sys.exit(3)
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
     rtamd.set_device(gpu)
@@ -522,7 +672,7 @@ def main():
            for _ in range(args.steps)]          # each timed step's all-gather + repack (gather stream)
     nframe = [0]
 
-    def step(i=None, counters=None, spp=SPP, sc=None, cm=None):
+    def step(i=None, counters=None, spp=SPP, sc=None, cm=None, cmode=0):
         sc = scene if sc is None else sc
         cm = cam if cm is None else cm
         b = nframe[0] % nbuf
@@ -535,12 +685,12 @@ def main():
         if interleaved:
             rtamd.check(L.spt_scene_render_groups_async(sc.handle, C.byref(cm), colors[b].data_ptr(),
                                                         seeds0.data_ptr(), seeds.data_ptr(), pixels[b].data_ptr(),
-                                                        W, H, rank, world, 0, spp, rtamd.SPT_PATH_TRACING, cptr,
-                                                        s.cuda_stream))
+                                                        W, H, rank, world, 0, spp, rtamd.SPT_PATH_TRACING | cmode,
+                                                        cptr, s.cuda_stream))
         else:
             rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cm), colors[b].data_ptr(),
                                                  seeds0.data_ptr(), seeds.data_ptr(), pixels[b].data_ptr(), W, H,
-                                                 r0, r1, 0, spp, rtamd.SPT_PATH_TRACING, cptr, s.cuda_stream))
+                                                 r0, r1, 0, spp, rtamd.SPT_PATH_TRACING | cmode, cptr, s.cuda_stream))
         if i is not None:
             ev[i][1].record(s)
         if world > 1:            # RCCL all-gather of the HDR bands + RGBA8 repack
@@ -673,9 +823,12 @@ def main():
         c4s, c4n, c4cam = rtamd.scenes.complex10k()
         rtamd.scenes.update_camera(c4cam, W, H)
         c4scene = rtamd.SmallptScene(c4s, c4n)
-        out["configs4_tiled"] = tiled_line(step, cnt, dev, world, distributed,
-                                           "configs[4]: 10k-sphere scene_build_complex, 1920x1080, 64 spp", SPP,
-                                           warm=2, sc=c4scene, cm=c4cam)
+        c4work = "configs[4]: 10k-sphere scene_build_complex, 1920x1080, 64 spp"
+        if world > 1:
+            out["configs4_tiled"] = list_tiled_line(dev, rank, world, distributed, s, c4scene, c4cam, SPP, c4work)
+        else:
+            out["configs4_tiled"] = tiled_line(step, cnt, dev, world, distributed, c4work, SPP, warm=2,
+                                               sc=c4scene, cm=c4cam, mode=rtamd.SPT_COUNT_RAYS)
     if rank == 0 and world == 1:
         if not args.no_whitted:
             out["whitted"] = whitted_line(args, dev)

@@ -135,6 +135,13 @@ int rtw_render_ocl_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xr
 /* ------------------------------------------------------------ smallpt */
 #define SPT_PATH_TRACING 0       /* RadiancePathTracing    geomfunc.h:167-338 */
 #define SPT_DIRECT_LIGHTING 1    /* RadianceDirectLighting geomfunc.h:340-483 */
+/* Flag OR-ed into `mode` of the device-resident entry points: with
+ * d_counters, count only counters[0] (Intersect calls), [1] (IntersectP
+ * calls) and [3] (samples) -- SURVEY §8(d)'s rays -- and leave counters[2]
+ * (sphere tests) untouched.  The sphere-test count needs IntersectP's
+ * early-exit position (geomfunc.h:94-110: the highest-index occluder), which
+ * costs hierarchy scenes a longer shadow walk; the call counts do not. */
+#define SPT_COUNT_RAYS 0x100
 
 /* Blocking, host buffers, whole frame.  Runs samples first_sample ..
  * first_sample+nsamples-1 of every pixel, exactly as nsamples successive
@@ -193,6 +200,37 @@ int spt_scene_render_groups_async(const spt_scene *scene, const rt_camera *camer
                                   int w, int h, int group, int ngroups, int first_sample, int nsamples,
                                   int mode, uint64_t *d_counters, void *stream);
 
+/* Tile groups: group g is the 8x8-pixel tiles 4g .. 4g+3 of the frame in
+ * row-major tile order (ceil(w/8) tiles per row) -- a 32x8 strip when
+ * ceil(w/8) is a multiple of 4.  spt_group_count(w, h) = ceil(ceil(w/8) *
+ * ceil(h/8) / 4) (or a negative RT_ERR_*). */
+int spt_group_count(int w, int h);
+
+/* spt_scene_render_async over an explicit set of tile groups: d_groups
+ * (device, ngroups DISTINCT entries in [0, spt_group_count(w, h)); entries
+ * outside are skipped) in dispatch order -- the first ones start first, so
+ * list the costliest first.  A multi-GPU frame split by per-rank lists
+ * balanced on measured costs (rtamd.dist.balanced_partition).  d_group_cost
+ * (nullable, device, spt_group_count(w, h) words; hierarchy scenes only,
+ * left unchanged otherwise): each listed group's wave time in 100 MHz ticks
+ * is ADDED to its entry (zero it first).  No order is learnt on this path.
+ * Same results per pixel as any other window. */
+int spt_scene_render_list_async(const spt_scene *scene, const rt_camera *camera, float *d_colors,
+                                const uint32_t *d_seeds_in, uint32_t *d_seeds_out, uint32_t *d_pixels,
+                                int w, int h, const int *d_groups, int ngroups, int first_sample,
+                                int nsamples, int mode, uint64_t *d_counters, unsigned *d_group_cost,
+                                void *stream);
+
+/* The accumulator of listed tile groups to / from a packed buffer of 768
+ * floats per group (its four tiles in turn, 64 pixels each in row-major
+ * order, r g b; pixels outside the frame pack as 0 and are not unpacked):
+ * the exchange of a frame split by group lists (one all-gather of the packed
+ * shares).  Exact copies, asynchronous on `stream`. */
+int spt_groups_pack_async(const float *d_colors, int w, int h, const int *d_groups, int ngroups,
+                          float *d_out, void *stream);
+int spt_groups_unpack_async(float *d_colors, int w, int h, const int *d_groups, int ngroups,
+                            const float *d_in, void *stream);
+
 /* The toInt pack of UpdateRenderingCPU (smallptCPU.cpp:120-122, vec.h:62)
  * alone: d_pixels[y*w+x] for rows [row_begin,row_end) from the accumulator
  * slots (h-y-1)*w+x of d_colors -- the pixels a render call writes, rebuilt
@@ -204,7 +242,9 @@ int spt_pack_pixels_async(const float *d_colors, uint32_t *d_pixels, int w, int 
 /* ------------------------------------------------------------ smallpt, several GPUs */
 /* One frame tiled over the GPUs of a node in row bands:
  * band k owns the k-th contiguous chunk of the flipped colour / seed slots,
- * i.e. pixel rows [h - e_k, h - s_k) with s_k = k*h/ngpus, e_k = (k+1)*h/ngpus.
+ * i.e. pixel rows [h - e_k, h - s_k) with B = ceil(h/ngpus), s_k = min(h, k*B),
+ * e_k = min(h, (k+1)*B) -- equal bands (the last one shorter, or empty), so
+ * one in-place all-gather of B rows per band assembles the frame.
  * Every pixel keeps its RNG words and accumulator on its band's device, so
  * rendering needs no exchange; samples of a pixel are never split.  One host
  * thread drives all devices (one stream each), as the reference's single
@@ -234,10 +274,10 @@ int spt_multi_render_async(spt_multi *m, const rt_camera *camera, int first_samp
                            int mode, int counters);
 /* Assembles the whole HDR accumulator on every band's device and repacks
  * each device's RGBA8 frame from it (spt_pack_pixels_async).  Distinct
- * devices: one RCCL group (ncclGroupStart / one ncclBroadcast per band /
- * ncclGroupEnd) over xGMI; repeated devices or RT_SPT_GATHER=peer: stream-
- * ordered peer copies (RT_SPT_GATHER=rccl runs the RCCL group even for a
- * single band).  Asynchronous. */
+ * devices: one in-place ncclAllGather of the equal (padded) bands over xGMI
+ * (the padding rows past h are never read); repeated devices or
+ * RT_SPT_GATHER=peer: stream-ordered peer copies (RT_SPT_GATHER=rccl runs the
+ * RCCL all-gather even for a single band).  Asynchronous. */
 int spt_multi_gather_async(spt_multi *m);
 /* Waits for every band's device work. */
 int spt_multi_sync(spt_multi *m);

@@ -989,8 +989,10 @@ extern "C" int rtq_render_async(const rtq_primitive *d_prims, int nprims, uint32
         if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render_async fork");
     }
     unsigned long long *cnt = (unsigned long long *)d_counters;
+    // (after the fork, an error return still joins the second stream back)
+    const auto bail = [&](int code) { return nstream == 2 ? rtrt::join_aux_on_error(*st, s, code) : code; };
     for (int i = 0; i < nstream; i++) {
-        if ((rc = arena(*st, i ? SLOT_Q2 : SLOT_Q, w, slab_rows, &A[i]))) return rc;
+        if ((rc = arena(*st, i ? SLOT_Q2 : SLOT_Q, w, slab_rows, &A[i]))) return bail(rc);
         A[i].row_stride = (int)nslab;
         hipLaunchKernelGGL(rt::queue::scene_kernel, dim3(1), dim3(64), 0, ss[i], d_prims, nprims,
                            (rt::queue::Scene *)A[i].scene);
@@ -1008,19 +1010,19 @@ extern "C" int rtq_render_async(const rtq_primitive *d_prims, int nprims, uint32
         hipError_t e = hipMemsetAsync(a.count, 0, sizeof(int) * rt::queue::C_TOTAL * rt::lq::CSTRIDE, sk);
         if (e == hipSuccess) e = hipMemsetAsync(a.fixbits, 0, sizeof(unsigned) * (((size_t)a.ntrees + 31) / 32), sk);
         if (e == hipSuccess) e = hipMemsetAsync(a.pixbits, 0, sizeof(unsigned) * (((size_t)a.npix + 31) / 32), sk);
-        if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render_async memset");
+        if (e != hipSuccess) return bail(rtrt::fail_hip(e, "rtq_render_async memset"));
         if (ex && *ex == '1')
             rc = cnt ? launch<true, true>(a, w, srows, row_end, DX, DY, cnt, sk, d_pixels)
                      : launch<false, true>(a, w, srows, row_end, DX, DY, cnt, sk, d_pixels);
         else
             rc = cnt ? launch<true, false>(a, w, srows, row_end, DX, DY, cnt, sk, d_pixels)
                      : launch<false, false>(a, w, srows, row_end, DX, DY, cnt, sk, d_pixels);
-        if (rc) return rc;
+        if (rc) return bail(rc);
     }
     if (nstream == 2) {
         hipError_t e = hipEventRecord(st->join_ev, st->aux);
         if (e == hipSuccess) e = hipStreamWaitEvent(s, st->join_ev, 0);
-        if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render_async join");
+        if (e != hipSuccess) return bail(rtrt::fail_hip(e, "rtq_render_async join"));
     }
     hipError_t e = hipEventRecord(st->wf_done, s);
     if (e != hipSuccess) return rtrt::fail_hip(e, "rtq_render_async record");

@@ -22,11 +22,11 @@ void release_state(DeviceState *st)
     if (!st) return;
     (void)hipSetDevice(st->device);
     if (st->stream) (void)hipStreamSynchronize(st->stream);
+    if (st->aux) (void)hipStreamSynchronize(st->aux);     // slabs of a frame that failed before its join
     if (st->wf_done) (void)hipEventSynchronize(st->wf_done);
     for (int i = 0; i < NSCRATCH; i++)
         if (st->buf[i]) (void)hipFree(st->buf[i]);
     if (st->pool_ovf) (void)hipHostFree(st->pool_ovf);   // host-mapped overflow flags
-    if (st->aux) (void)hipStreamSynchronize(st->aux);
     if (st->wf_done) (void)hipEventDestroy(st->wf_done);
     if (st->fork_ev) (void)hipEventDestroy(st->fork_ev);
     if (st->join_ev) (void)hipEventDestroy(st->join_ev);
@@ -50,6 +50,19 @@ int aux_stream(DeviceState &st)
         return fail_hip(e, "aux stream");
     }
     return RT_OK;
+}
+
+int join_aux_on_error(DeviceState &st, hipStream_t s, int rc)
+{
+    // Work already queued on aux keeps running: the caller's stream (and the
+    // next frame, through wf_done) must still wait for it.  The error text
+    // of rc is kept (rt_last_error).
+    if (st.aux && hipEventRecord(st.join_ev, st.aux) == hipSuccess &&
+        hipStreamWaitEvent(s, st.join_ev, 0) == hipSuccess && hipEventRecord(st.wf_done, s) == hipSuccess)
+        st.wf_pending = true;
+    else if (st.aux)
+        (void)hipStreamSynchronize(st.aux);
+    return rc;
 }
 
 int fail(int code, const char *msg)
@@ -129,6 +142,7 @@ int scratch(DeviceState &st, int slot, size_t bytes, void **out)
     if (st.cap[slot] < bytes) {
         if (st.buf[slot]) {
             hipError_t e = hipStreamSynchronize(st.stream);
+            if (e == hipSuccess && st.aux) e = hipStreamSynchronize(st.aux);
             if (e != hipSuccess) return fail_hip(e, "scratch sync");
             (void)hipFree(st.buf[slot]);
             st.cached_bytes -= st.cap[slot];

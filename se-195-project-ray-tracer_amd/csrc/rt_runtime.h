@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <mutex>
 #include <stddef.h>
+#include <string>
 #include "../../include/rt_hip.h"
 
 namespace rtrt {
@@ -70,11 +71,19 @@ int scratch(DeviceState &st, int slot, size_t bytes, void **out);
 double pool_fraction(DeviceState &st, int which, long long trees, double initial, int **flag_dev);
 // The state's second stream and its fork / join events (created on first use).
 int aux_stream(DeviceState &st);
+// An error after a frame forked work onto aux: joins aux back into s (and
+// records wf_done, so the next frame and any buffer regrowth wait for it);
+// returns rc.
+int join_aux_on_error(DeviceState &st, hipStream_t s, int rc);
 // Frees the per-device scenes cached by spt_render / spt_render_async
 // (smallpt.hip; rt_release).
 void release_cached_scenes();
 // Frees spt_render_multi's cached band context (spt_multi.hip; rt_release).
 void release_cached_multi();
+// The environment knobs spt_scene_create reads (RT_SPT_NO_BVH, RT_SPT_GEO,
+// RT_SPT_WIDE, RT_SPT_WIDE_LEAF, RT_WIDE_WPB) as one key: the scene caches
+// of spt_render and spt_render_multi rebuild when it changes (smallpt.hip).
+std::string scene_prep_hooks();
 // The calling thread's rt_set_device choice (-1: none, HIP's current device).
 int thread_device();
 // Saves the calling thread's device selection (rt_set_device and HIP's

@@ -1174,7 +1174,10 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
     return done;
 }
 
-struct Counts { unsigned long long isect, isectp, tests, samples; };
+// Per-lane work counters: calls and samples in 32 bits (a lane adds a few per
+// sample; render_kernel flushes a lane's calls with an atomic before they
+// could wrap), sphere tests in 64.  Four VGPRs fewer than four u64 words.
+struct Counts { unsigned isect, isectp, samples; unsigned long long tests; };
 
 // Tools-only block profile (build with -DRT_SPT_PROF; tools/ab.py PROF=1):
 // per code block, the lanes that executed it and the wave-executions
@@ -1259,15 +1262,19 @@ constexpr int GS_BYTES = 6160;      // per tile group: 8 x 96 colour floats, 8 x
 // the next iteration queries both (query2_bf) and applies the shadow result
 // (rad += thr * Ld, geomfunc.h:229-230) before it shades the bounce's hit.
 // One iteration per path vertex instead of two for a lit DIFF vertex.
-template <bool DL, bool COUNT, int GEO, bool DUAL = false>
-__global__ void __launch_bounds__(1024, GEO == 2 ? (COUNT ? RT_BVH_MINWAVES_COUNT : RT_BVH_MINWAVES)
-                                              : GEO == 3 ? (COUNT ? RT_BVH_MINWAVES_COUNT : RT_WIDE_MINWAVES)
-                                              : ((DUAL && !COUNT) ? RT_SPT_DUAL_MINWAVES : RT_SPT_MINWAVES))
+// COUNT: all four counters (the sphere-test count needs IntersectP's early-
+// exit position, so a counted shadow query finds the highest-index
+// occluder).  RAYS (SPT_COUNT_RAYS): Intersect / IntersectP calls and samples
+// only, with the uncounted queries (any occluder ends a shadow query).
+template <bool DL, bool COUNT, int GEO, bool DUAL = false, bool RAYS = false>
+__global__ void __launch_bounds__(1024, GEO == 2 ? ((COUNT || RAYS) ? RT_BVH_MINWAVES_COUNT : RT_BVH_MINWAVES)
+                                              : GEO == 3 ? ((COUNT || RAYS) ? RT_BVH_MINWAVES_COUNT : RT_WIDE_MINWAVES)
+                                              : ((DUAL && !COUNT && !RAYS) ? RT_SPT_DUAL_MINWAVES : RT_SPT_MINWAVES))
 render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,
               uint32_t *seeds_out, uint32_t *__restrict__ pixels, int w, int h,
-              int row_begin, int row_end, int tiles_x, int ntiles, int gstride, int first_sample, int nsamples,
-              int prio_sched, const int *__restrict__ group_order, unsigned *__restrict__ group_cost,
+              int row_begin, int row_end, int tiles_x, int ntiles, int nslots, int gstride, int first_sample,
+              int nsamples, int prio_sched, const int *__restrict__ group_order, unsigned *__restrict__ group_cost,
               const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
               const float4 *__restrict__ g_col, const float4 *__restrict__ g_lrec, int nlights,
               BvhView bvh, unsigned long long *__restrict__ counters, int *__restrict__ work, int split,
@@ -1322,6 +1329,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // (Cornell) the order/cost plumbing cost 1.4 % of the frame and 8 % of an
     // N = 8 band (measured A/B) although it is never used there.
     constexpr bool SCHED = GEO == GEO_BVH || GEO == GEO_WIDE;
+    constexpr bool CALLS = COUNT || RAYS;           // the call / sample counters are kept
     Counts cnt = {0, 0, 0, 0};
 #ifdef RT_SPT_PROF
     unsigned prof_l[PB_N] = {}, prof_w[PB_N] = {};
@@ -1336,7 +1344,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     const int hs = PERSIST ? (split & 3) : 0;
     // waves of a block that take tier-1 sub-items first (split bits 3..7; 0: 4 << hs)
     const int hw = ((split >> 3) & 31) ? ((split >> 3) & 31) : (4 << hs);
-    const int nitems = 4 * ((ntiles + 3) >> 2);
+    const int nitems = 4 * nslots;
     // Three tiers, in dispatch order (heaviest first with a learnt order):
     // nheavy bits 0..15 = n1 tiles split into 2^hs sub-items each (the
     // cooperative walk with split bit 2), bits 16..31 = n2 tiles routed one
@@ -1380,7 +1388,11 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     const int item = heavy_ ? f >> hs : f - (n1 << hs) + n1;
     const int sub = heavy_ ? f & ((1 << hs) - 1) : 0;
     const int slot = item >> 2;
-    const int grp = (SCHED && group_order) ? group_order[slot] : slot;
+    // group_order: the learnt order (hierarchy kernels) or the caller's
+    // group list (spt_scene_render_list_async, every kernel) of nslots
+    // entries; a slot past it or an entry outside the frame renders nothing.
+    const int grp = group_order ? (slot < nslots ? group_order[slot] : -1) : slot;
+    const bool gvalid = (unsigned)grp < (unsigned)((ntiles + 3) >> 2);
     const int tile = grp * 4 + (item & 3);
     const int li = coop ? (sub << (6 - hs)) + (cg == 8 ? lane >> 3 : lane >> 2)   // pixel of the 8x8 tile
                         : (sub << (6 - sp_)) + lane;    //   (valid: lane < 64 >> split)
@@ -1401,13 +1413,13 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // (spt_scene_render_groups_async, multi-GPU load balance).
     const int y = row_begin + (tile / tiles_x) * 8 * gstride + (li >> 3);
 #ifdef RT_SPT_TRACE
-    const bool active = lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end &&
+    const bool active = gvalid && lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end &&
                         (g_spt_only_group < 0 || grp == g_spt_only_group);
     unsigned tr_walk = 0, tr_leaf = 0, tr_trips = 0, tr_leafruns = 0, tr_queries = 0;
     const unsigned long long tr_c0 = __builtin_amdgcn_s_memtime();
     const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();
 #else
-    const bool active = lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end;
+    const bool active = gvalid && lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end;
 #endif
 
 #ifdef RT_SPT_TRACE
@@ -1817,6 +1829,11 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                     col.z = (col.z * k1 + rad.z) * k2;
                 }
                 cnt.samples++;
+                if (CALLS && (cnt.isect | cnt.isectp) >= 0x80000000u) {   // (long launches: before 32 bits wrap)
+                    atomicAdd(counters, (unsigned long long)cnt.isect);
+                    atomicAdd(counters + 1, (unsigned long long)cnt.isectp);
+                    cnt.isect = cnt.isectp = 0;
+                }
                 k++;
                 need_cam = k < nsamples;
                 fin = false;
@@ -1878,7 +1895,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 const int tl = grp * 4 + (c >> 3);
                 xx = (tl % tiles_x) * 8 + (c & 7);
                 yy = row_begin + (tl / tiles_x) * 8 * gstride + r;
-                return tl < ntiles && xx < w && yy < row_end;
+                return gvalid && tl < ntiles && xx < w && yy < row_end;
             };
             int xx, yy;
             if (nsamples > 0) {
@@ -1901,7 +1918,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         }
     }
 #undef GS_BASE
-    if (SCHED && group_cost && lane == 0)   // this tile's duration (100 MHz ticks), summed per group
+    if (SCHED && group_cost && gvalid && lane == 0)   // this tile's duration (100 MHz ticks), summed per group
         atomicAdd(&group_cost[grp], (unsigned)(__builtin_amdgcn_s_memrealtime() - t_start));
 #ifdef RT_SPT_TRACE
     {
@@ -1926,17 +1943,17 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         }
     }
 #endif
-    if (COUNT && PERSIST && (split & 4)) {              // a cooperative group counts its pixel once:
+    if (CALLS && PERSIST && (split & 4)) {              // a cooperative group counts its pixel once:
         if (!lead) cnt = Counts{0, 0, 0, 0};            //   flushed per work item
-        const unsigned long long c[4] = {cnt.isect, cnt.isectp, cnt.tests, cnt.samples};
+        const unsigned long long c[4] = {cnt.isect, cnt.isectp, COUNT ? cnt.tests : 0ull, cnt.samples};
         flush_counters<4>(counters, c);
         cnt = Counts{0, 0, 0, 0};
     }
     if (!PERSIST) break;
     f = __builtin_amdgcn_readfirstlane(fetch());
     }   // work items
-    if (COUNT) {
-        const unsigned long long c[4] = {cnt.isect, cnt.isectp, cnt.tests, cnt.samples};
+    if (CALLS) {
+        const unsigned long long c[4] = {cnt.isect, cnt.isectp, COUNT ? cnt.tests : 0ull, cnt.samples};
         flush_counters<4>(counters, c);
     }
 #ifdef RT_SPT_PROF
@@ -1960,6 +1977,32 @@ __global__ void __launch_bounds__(256) pack_kernel(const float *__restrict__ col
         const size_t i = (size_t)(h - y - 1) * w + x;
         pixels[(size_t)y * w + x] =
             (uint32_t)(to_int(colors[3 * i]) | (to_int(colors[3 * i + 1]) << 8) | (to_int(colors[3 * i + 2]) << 16));
+    }
+}
+
+// Tile groups <-> a packed buffer (a multi-GPU frame split by explicit group
+// lists, spt_groups_pack_async): group g is the 8x8 tiles 4g .. 4g+3 of the
+// frame in row-major tile order; its 768 packed floats are tile by tile, row
+// by row, pixel by pixel, (r, g, b) -- the accumulator slots (h-y-1)*w+x.
+// Pixels outside the frame (and entries outside [0, ngroups_total)) pack as
+// 0 and are skipped when unpacking.  Exact copies.
+constexpr int GROUP_FLOATS = 4 * 64 * 3;
+template <bool PACK>
+__global__ void __launch_bounds__(256) groups_copy_kernel(float *__restrict__ colors, int w, int h,
+                                                          const int *__restrict__ groups, int n,
+                                                          float *__restrict__ buf)
+{
+    const int tiles_x = (w + 7) / 8, ntiles = tiles_x * ((h + 7) / 8), total = (ntiles + 3) / 4;
+    const size_t ne = (size_t)n * GROUP_FLOATS;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += (size_t)gridDim.x * blockDim.x) {
+        const int k = (int)(e / GROUP_FLOATS), q = (int)(e % GROUP_FLOATS);
+        const int g = groups[k];
+        const int tile = g * 4 + q / 192, p = (q % 192) / 3, comp = q % 3;
+        const int x = (tile % tiles_x) * 8 + (p & 7), y = (tile / tiles_x) * 8 + (p >> 3);
+        const bool in = (unsigned)g < (unsigned)total && tile < ntiles && x < w && y < h;
+        const size_t i = 3 * ((size_t)(h - 1 - y) * w + x) + comp;
+        if (PACK) buf[e] = in ? colors[i] : 0.f;
+        else if (in) colors[i] = buf[e];
     }
 }
 
@@ -2016,9 +2059,13 @@ struct spt_scene {
     // Work counters of the persistent (8-wide hierarchy) launches: a ring,
     // one zeroed quad (rest, routed heavy, cooperative, unused) per launch, so
     // launches in flight on several streams do not share one.
+    // An entry a stream capture used is baked into that graph, which may be
+    // replayed at any time: it is never handed out again (work_captured).
     static constexpr int NWORK = 64;
     int *d_work = nullptr;
     mutable int work_next = 0;
+    mutable unsigned long long work_captured = 0;
+    int wide_wpb = 16;                // waves per block of the 8-wide launches (fixed at build: the LDS fit)
 };
 
 namespace {
@@ -2048,41 +2095,46 @@ namespace {
 // SIMD gets four waves, instead of the dispatcher's uneven 3..5 per SIMD.
 struct Shape {
     int tiles_x, ntiles, gstride, wpb, nblocks;
+    int work = 0;                     // tiles this launch renders (ntiles, or 4 x a group list's length)
     int nslots = 0;                   // dispatch slots (tile groups of four) the order / cost arrays cover
     const int *order = nullptr;       // adaptive schedule (render_kernel's group_order / group_cost)
     unsigned *cost = nullptr;
     int heavy16 = 0;                  // with order: heaviest slots kept at top priority, in 16s
+    bool tiers = true;                // with order: its first tiles get the heavy-tile treatment
 };
 // Rows [r0, r1), or (gstride > 1) the 8-row groups r0/8, r0/8 + gstride, ...
-// below r1 (r0 a multiple of 8).
-Shape launch_shape(const spt_scene &sc, int w, int r0, int r1, int gstride = 1)
+// below r1 (r0 a multiple of 8); or (nlist > 0) the nlist tile groups of a
+// caller's list over the frame [r0, r1) = [0, h).
+Shape launch_shape(const spt_scene &sc, int w, int r0, int r1, int gstride = 1, int nlist = 0)
 {
     Shape g;
     g.tiles_x = (w + 7) / 8;
     g.gstride = gstride;
     const int groups = (r1 - r0 + 7) / 8;
     g.ntiles = g.tiles_x * ((groups + gstride - 1) / gstride);
+    const int work = nlist > 0 ? 4 * nlist : g.ntiles;      // tiles this launch renders
+    g.work = work;
     // Waves of work per SIMD: up to 4 (an N = 8 band) run as one round of the
     // 16-wave block shape (four waves per SIMD, one block per CU); 6..8 (an
     // N = 4 band: 7.97) as two such rounds -- at occupancy 6 they run as a
     // full round of 6 and a tail of 2 (N = 4 bands 5.25-5.87 ms -> 5.44-5.47
     // ms); otherwise 256-thread blocks at the kernel's occupancy.
-    const double wps = (double)g.ntiles / (4.0 * sc.cus);
+    const double wps = (double)work / (4.0 * sc.cus);
     g.wpb = (wps <= 4.0 || (wps > 6.0 && wps <= 8.0)) ? 16 : 4;
     if (const char *e = getenv("RT_SPT_WPB")) g.wpb = atoi(e) == 16 ? 16 : 4;   // A/B
-    g.nblocks = (g.ntiles + g.wpb - 1) / g.wpb;
-    g.nslots = g.nblocks * (g.wpb / 4);
+    g.nblocks = (work + g.wpb - 1) / g.wpb;
+    g.nslots = nlist > 0 ? nlist : g.nblocks * (g.wpb / 4);
     if (sc.bvh.wnode) {               // persistent waves: one block per CU (fewer for a small window)
-        g.wpb = wide_wpb();
-        g.nblocks = (g.ntiles + g.wpb - 1) / g.wpb;
-        g.nslots = (g.ntiles + 3) / 4;
+        g.wpb = sc.wide_wpb;
+        g.nblocks = (work + g.wpb - 1) / g.wpb;
+        g.nslots = nlist > 0 ? nlist : (g.ntiles + 3) / 4;
 #if RT_WIDE_PERSIST
         g.nblocks = std::min(sc.cus, g.nblocks);
         if (const char *e = getenv("RT_WIDE_BLOCKS")) g.nblocks = std::max(1, atoi(e));   // A/B
 #else
         g.wpb &= ~3;                  // static: whole groups per block, a slot per group
-        g.nblocks = (g.ntiles + g.wpb - 1) / g.wpb;
-        g.nslots = g.nblocks * (g.wpb / 4);
+        g.nblocks = (work + g.wpb - 1) / g.wpb;
+        g.nslots = nlist > 0 ? nlist : g.nblocks * (g.wpb / 4);
 #endif
     }
     return g;
@@ -2101,10 +2153,28 @@ int prio_schedule(const Shape &g)
     return (a & 255) | ((b & 255) << 8) | ((c & 255) << 16) | ((g.order ? g.heavy16 & 255 : 0) << 24);
 }
 
-template <bool DL, bool COUNT, int GEO, bool DUAL = false>
-void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &cam, float *colors,
-            const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h, int r0, int r1,
-            int first, int ns, unsigned long long *cnt)
+// A zeroed work-counter quad of the scene's ring for one persistent launch
+// on `s` (nullptr + rt error: none left).
+int *work_entry(const spt_scene &sc, hipStream_t s)
+{
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const bool capturing = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+    for (int tries = 0; tries < spt_scene::NWORK; tries++) {
+        const int k = sc.work_next++ % spt_scene::NWORK;
+        if ((sc.work_captured >> k) & 1ull) continue;
+        if (capturing) sc.work_captured |= 1ull << k;
+        int *work = sc.d_work + 4 * k;
+        if (hipMemsetAsync(work, 0, 4 * sizeof(int), s) != hipSuccess) return nullptr;   // (check_launch reports it)
+        return work;
+    }
+    rtrt::fail(RT_ERR_INVALID, "spt render: every work-counter entry of the scene is held by a captured graph");
+    return nullptr;
+}
+
+template <bool DL, bool COUNT, int GEO, bool DUAL = false, bool RAYS = false>
+int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &cam, float *colors,
+           const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h, int r0, int r1,
+           int first, int ns, unsigned long long *cnt)
 {
     constexpr bool LDS = GEO == rt::smallpt::GEO_LDS;
     const int n = sc.n;
@@ -2115,8 +2185,7 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     int *work = nullptr;
     if (GEO == rt::smallpt::GEO_WIDE) {
         lds = wide_lds_bytes(sc.bvh.wnodes, sc.bvh.wdepth, g.wpb, COUNT);
-        work = sc.d_work + 4 * (sc.work_next++ % spt_scene::NWORK);
-        if (hipMemsetAsync(work, 0, 4 * sizeof(int), s) != hipSuccess) return;   // (check_launch reports it)
+        if (!(work = work_entry(sc, s))) return rtrt::check_launch("spt work counters") ? RT_ERR_HIP : RT_ERR_INVALID;
     }
     // Heavy tiles (with a learnt order, GEO_WIDE persistent launches), in
     // dispatch order: n1 cooperative tiles (RT_SPT_COOP_G lanes per pixel,
@@ -2129,9 +2198,9 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
     // configs[4], 64 spp (profiles/r03/c4_coop_*.log): N = 8 windows
     // 18.0-19.8 -> 11.4-15.1 ms, N = 4 18.7 -> 17 ms; see DESIGN.md.
     int n1 = 0, n2 = 0, sp = 0;
-    if (GEO == rt::smallpt::GEO_WIDE && RT_WIDE_PERSIST && g.order) {
+    if (GEO == rt::smallpt::GEO_WIDE && RT_WIDE_PERSIST && g.order && g.tiers) {
         n2 = std::min(4 * g.nblocks, 4 * g.nslots);
-        const double wps = (double)g.ntiles / (4.0 * sc.cus);
+        const double wps = (double)g.work / (4.0 * sc.cus);
         int hw = 0;
         if (wps <= 5.0) {
             n1 = 2 * sc.cus;
@@ -2160,16 +2229,34 @@ void launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera 
         split = (RT_WIDE_PERSIST ? sp : 0) | (std::min(std::max(budget, 1), 255) << 8) |
                 (std::min(std::max(batch, 0), 64) << 16) | (std::min(std::max(stop, 0), 64) << 24);
     }
-    hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
-                       sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.gstride, first,
+    hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
+                       sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.nslots, g.gstride, first,
                        ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt, work, split,
                        nheavy);
+    return RT_OK;
+}
+
+// Counter modes of a launch: none, all four counters, or calls and samples
+// only (SPT_COUNT_RAYS: the uncounted queries).
+enum { CNT_NONE = 0, CNT_FULL = 1, CNT_RAYS = 2 };
+
+template <int GEO, bool DL, bool DUAL>
+int launch_counted(int cmode, const Shape &grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam,
+                   float *colors, const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h, int r0,
+                   int r1, int first, int ns, unsigned long long *cnt)
+{
+    if (cmode == CNT_FULL)
+        return launch<DL, true, GEO, DUAL>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+    if (cmode == CNT_RAYS)
+        return launch<DL, false, GEO, DUAL, true>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns,
+                                                  cnt);
+    return launch<DL, false, GEO, DUAL>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
 }
 
 template <int GEO>
-void launch_mode(bool dl, bool count, const Shape &grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam,
-                 float *colors, const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h,
-                 int r0, int r1, int first, int ns, unsigned long long *cnt)
+int launch_mode(bool dl, int cmode, const Shape &grid, hipStream_t s, const spt_scene &sc, const rt_camera &cam,
+                float *colors, const uint32_t *sin, uint32_t *sout, uint32_t *pixels, int w, int h,
+                int r0, int r1, int first, int ns, unsigned long long *cnt)
 {
     // The two-query iteration for path tracing in single-light scenes, at
     // every launch shape: one iteration per lit DIFF vertex instead of two.
@@ -2177,18 +2264,20 @@ void launch_mode(bool dl, bool count, const Shape &grid, hipStream_t s, const sp
     // state reset at sample end) it fits 72 VGPRs at occupancy 7 and beats
     // the one-query form both where per-wave ILP is short (N = 8 band) and on
     // the full frame (17.98 -> 17.3 ms).  RT_SPT_DUAL=0 / 1 forces it off / on (A/B).
+    // (The hierarchy walks keep the one-query form: their two resumable
+    // walks in one loop spill)
     const int dual_env = getenv("RT_SPT_DUAL") ? atoi(getenv("RT_SPT_DUAL")) : -1;
     const bool dual_ok = dual_env != 0;
-    if (dl) {
-        if (count) launch<true, true, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
-        else launch<true, false, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
-    } else if (GEO != rt::smallpt::GEO_BVH && GEO != rt::smallpt::GEO_WIDE && sc.nlights == 1 && dual_ok) {
-        if (count) launch<false, true, GEO, true>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
-        else launch<false, false, GEO, true>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
-    } else {
-        if (count) launch<false, true, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
-        else launch<false, false, GEO>(grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first, ns, cnt);
+    if (dl)
+        return launch_counted<GEO, true, false>(cmode, grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1,
+                                                first, ns, cnt);
+    if constexpr (GEO != rt::smallpt::GEO_BVH && GEO != rt::smallpt::GEO_WIDE) {
+        if (sc.nlights == 1 && dual_ok)
+            return launch_counted<GEO, false, true>(cmode, grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1,
+                                                    first, ns, cnt);
     }
+    return launch_counted<GEO, false, false>(cmode, grid, s, sc, cam, colors, sin, sout, pixels, w, h, r0, r1, first,
+                                             ns, cnt);
 }
 
 // ---- hierarchy build (host, spt_bvh.h) for scenes of >= sptbvh::MIN_SPHERES spheres
@@ -2219,10 +2308,11 @@ int build_scene_bvh(spt_scene *sc, const rt_sphere *spheres)
     if (nn && !(we && atoi(we) == 0)) {
         int first = 8;                                  // RT_SPT_WIDE_LEAF: A/B of the leaf size
         if (const char *e = getenv("RT_SPT_WIDE_LEAF")) first = std::min(std::max(atoi(e), 1), 16);
+        sc->wide_wpb = wide_wpb();                      // (RT_WIDE_WPB: A/B) read once, here
         for (int lm : {first, 8, 12, 16}) {
             wb.leaf_max = lm;
             wb.build(b);
-            if (wide_lds_bytes(wb.nnodes, wb.depth, wide_wpb()) <= WIDE_LDS_MAX) { wide = true; break; }
+            if (wide_lds_bytes(wb.nnodes, wb.depth, sc->wide_wpb) <= WIDE_LDS_MAX) { wide = true; break; }
         }
     }
     std::vector<float4> geo(nb + na);
@@ -2272,7 +2362,8 @@ int check_render_args(const rt_camera *camera, float *d_colors, const uint32_t *
         return rtrt::fail(RT_ERR_INVALID, "spt render: bad sizes");
     if (row_begin < 0 || row_end > h || row_begin > row_end)
         return rtrt::fail(RT_ERR_INVALID, "spt render: bad row range");
-    if (mode != SPT_PATH_TRACING && mode != SPT_DIRECT_LIGHTING)
+    const int base = mode & ~SPT_COUNT_RAYS;
+    if (base != SPT_PATH_TRACING && base != SPT_DIRECT_LIGHTING)
         return rtrt::fail(RT_ERR_INVALID, "spt render: bad mode");
     return RT_OK;
 }
@@ -2357,7 +2448,7 @@ namespace {
 // Adaptive order (SptSched) for one launch: sets g.order / g.cost; returns
 // true if the caller must queue the cost read-back after the launch.
 bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, int r0, int r1, int gstride,
-                  int ns, int mode, const rt_camera &cam)
+                  int ns, int mode, const rt_camera &cam, bool full_count)
 {
     const char *e = getenv("RT_SPT_SCHED");
     if (!sc.bvh.node || (e && atoi(e) == 0)) return false;   // the full-scan kernels have no order/cost code
@@ -2425,7 +2516,12 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
         g.heavy16 = std::min(std::max((heavy + 15) / 16, 0), 255);
         return false;
     }
-    if (q.state == 0) {
+    // A full-counter launch does not record: its shadow walks look for the
+    // highest-index occluder (twice the uncounted walk's work, unevenly
+    // over the tiles), so its tile costs would order the uncounted launches
+    // wrongly (configs[4]: 28.0 ms with such an order, 25.4 ms with the
+    // uncounted kernel's own).
+    if (q.state == 0 && !full_count) {
         if (hipMemsetAsync(q.d_cost, 0, sizeof(unsigned) * nslots, s) != hipSuccess) return false;
         g.cost = q.d_cost;
         return true;
@@ -2441,32 +2537,52 @@ void sched_after(const spt_scene &sc, hipStream_t s)
         q.state = 1;
 }
 
+// One launch of rows [row_begin, row_end) (every gstride-th 8-row group), or
+// (d_list) of the caller's nlist tile groups over the whole frame.
 int scene_render(const spt_scene *sc, const rt_camera *camera, float *d_colors, const uint32_t *d_seeds_in,
                  uint32_t *d_seeds_out, uint32_t *d_pixels, int w, int h, int row_begin, int row_end, int gstride,
-                 int first_sample, int nsamples, int mode, uint64_t *d_counters, void *stream)
+                 int first_sample, int nsamples, int mode, uint64_t *d_counters, void *stream,
+                 const int *d_list = nullptr, int nlist = 0, unsigned *d_cost = nullptr)
 {
-    if (row_begin >= row_end) return RT_OK;
-    Shape grid = launch_shape(*sc, w, row_begin, row_end, gstride);
+    if (row_begin >= row_end || (d_list && nlist < 1)) return RT_OK;
+    Shape grid = launch_shape(*sc, w, row_begin, row_end, gstride, d_list ? nlist : 0);
     hipStream_t s = (hipStream_t)stream;
-    const bool record = sched_before(*sc, grid, s, w, h, row_begin, row_end, gstride, nsamples, mode, *camera);
+    const int base = mode & ~SPT_COUNT_RAYS;
+    bool record = false;
+    if (d_list) {
+        // The caller's order, heaviest first: its first groups get the
+        // heavy-tile treatment (top priority, cooperative or routed tiles)
+        // as with a learnt order -- unless the launch records costs
+        // (d_cost): the list is then taken as unordered and every tile runs
+        // a lane per pixel, so the recorded costs compare like with like.
+        grid.order = d_list;
+        grid.cost = sc->bvh.node ? d_cost : nullptr;
+        grid.tiers = d_cost == nullptr;
+        grid.heavy16 = d_cost ? 0 : std::min(std::max((sc->cus / 4 + 15) / 16, 0), 255);
+    } else {
+        record = sched_before(*sc, grid, s, w, h, row_begin, row_end, gstride, nsamples, base, *camera,
+                              d_counters && !(mode & SPT_COUNT_RAYS));
+    }
     unsigned long long *cnt = (unsigned long long *)d_counters;
-    const bool dl = mode == SPT_DIRECT_LIGHTING;
+    const bool dl = base == SPT_DIRECT_LIGHTING;
+    const int cmode = !cnt ? CNT_NONE : (mode & SPT_COUNT_RAYS) ? CNT_RAYS : CNT_FULL;
+    int rc;
     if (sc->bvh.wnode)
-        launch_mode<rt::smallpt::GEO_WIDE>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in,
-                                           d_seeds_out, d_pixels, w, h, row_begin, row_end, first_sample,
-                                           nsamples, cnt);
+        rc = launch_mode<rt::smallpt::GEO_WIDE>(dl, cmode, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
+                                                d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
     else if (sc->bvh.node)
-        launch_mode<rt::smallpt::GEO_BVH>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in,
-                                          d_seeds_out, d_pixels, w, h, row_begin, row_end, first_sample,
-                                          nsamples, cnt);
-    else if ((size_t)(3 * sc->n + 3 * std::max(sc->nlights, 1)) * sizeof(float4) <= (size_t)rt::smallpt::MAX_LDS_BYTES &&
+        rc = launch_mode<rt::smallpt::GEO_BVH>(dl, cmode, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
+                                               d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
+    else if ((size_t)(3 * sc->n + 3 * std::max(sc->nlights, 1)) * sizeof(float4) <=
+                 (size_t)rt::smallpt::MAX_LDS_BYTES &&
              !sc->force_global)
-        launch_mode<rt::smallpt::GEO_LDS>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
-                             d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
+        rc = launch_mode<rt::smallpt::GEO_LDS>(dl, cmode, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
+                                               d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
     else
-        launch_mode<rt::smallpt::GEO_GLOBAL>(dl, cnt != nullptr, grid, s, *sc, *camera, d_colors, d_seeds_in, d_seeds_out,
-                              d_pixels, w, h, row_begin, row_end, first_sample, nsamples, cnt);
-    const int rc = rtrt::check_launch("spt render_kernel");
+        rc = launch_mode<rt::smallpt::GEO_GLOBAL>(dl, cmode, grid, s, *sc, *camera, d_colors, d_seeds_in,
+                                                  d_seeds_out, d_pixels, w, h, row_begin, row_end, first_sample,
+                                                  nsamples, cnt);
+    if (rc == RT_OK) rc = rtrt::check_launch("spt render_kernel");
     if (rc == RT_OK && record) sched_after(*sc, s);
     return rc;
 }
@@ -2500,6 +2616,64 @@ extern "C" int spt_scene_render_groups_async(const spt_scene *sc, const rt_camer
                         first_sample, nsamples, mode, d_counters, stream);
 }
 
+extern "C" int spt_group_count(int w, int h)
+{
+    if (w < 1 || h < 1) return rtrt::fail(RT_ERR_INVALID, "spt_group_count: bad size");
+    const long long n = ((long long)((w + 7) / 8) * ((h + 7) / 8) + 3) / 4;
+    if (n > (1LL << 28)) return rtrt::fail(RT_ERR_INVALID, "spt_group_count: frame too large");
+    return (int)n;
+}
+
+extern "C" int spt_scene_render_list_async(const spt_scene *sc, const rt_camera *camera, float *d_colors,
+                                           const uint32_t *d_seeds_in, uint32_t *d_seeds_out, uint32_t *d_pixels,
+                                           int w, int h, const int *d_groups, int ngroups, int first_sample,
+                                           int nsamples, int mode, uint64_t *d_counters, unsigned *d_group_cost,
+                                           void *stream)
+{
+    if (!sc) return rtrt::fail(RT_ERR_INVALID, "spt_scene_render_list_async: null scene");
+    const int total = spt_group_count(w, h);
+    if (total < 0) return total;
+    if (ngroups < 0 || ngroups > total || (ngroups > 0 && !d_groups))
+        return rtrt::fail(RT_ERR_INVALID, "spt_scene_render_list_async: need 0 <= ngroups <= spt_group_count(w, h)");
+    int rc = check_render_args(camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, 0, h, first_sample,
+                               nsamples, mode);
+    if (rc) return rc;
+    return scene_render(sc, camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, 0, h, 1, first_sample,
+                        nsamples, mode, d_counters, stream, d_groups, ngroups, d_group_cost);
+}
+
+namespace {
+int groups_copy(bool pack, float *d_colors, int w, int h, const int *d_groups, int n, float *d_buf, void *stream)
+{
+    const int total = spt_group_count(w, h);
+    if (total < 0) return total;
+    if (!d_colors || !d_buf || n < 0 || n > total || (n > 0 && !d_groups))
+        return rtrt::fail(RT_ERR_INVALID, "spt_groups_pack/unpack: bad arguments");
+    if (n == 0) return RT_OK;
+    const size_t ne = (size_t)n * rt::smallpt::GROUP_FLOATS;
+    const unsigned blocks = (unsigned)std::min<size_t>((ne + 255) / 256, 8192);
+    if (pack)
+        hipLaunchKernelGGL(rt::smallpt::groups_copy_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                           d_colors, w, h, d_groups, n, d_buf);
+    else
+        hipLaunchKernelGGL(rt::smallpt::groups_copy_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                           d_colors, w, h, d_groups, n, d_buf);
+    return rtrt::check_launch("spt groups_copy_kernel");
+}
+}  // namespace
+
+extern "C" int spt_groups_pack_async(const float *d_colors, int w, int h, const int *d_groups, int ngroups,
+                                     float *d_out, void *stream)
+{
+    return groups_copy(true, (float *)d_colors, w, h, d_groups, ngroups, d_out, stream);
+}
+
+extern "C" int spt_groups_unpack_async(float *d_colors, int w, int h, const int *d_groups, int ngroups,
+                                       const float *d_in, void *stream)
+{
+    return groups_copy(false, d_colors, w, h, d_groups, ngroups, (float *)d_in, stream);
+}
+
 namespace {
 // One prepared scene per device for the entry points that take a bare sphere
 // array (spt_render, spt_render_async), reused while the array is unchanged
@@ -2513,18 +2687,27 @@ struct SceneCache {
 };
 SceneCache g_scene_cache[64];
 
-std::string prep_hooks()
-{
-    const char *a = getenv("RT_SPT_NO_BVH"), *b = getenv("RT_SPT_GEO"), *c = getenv("RT_SPT_WIDE"),
-               *d = getenv("RT_SPT_WIDE_LEAF");
-    return std::string(a ? "1" : "0") + "|" + (b ? b : "") + "|" + (c ? c : "") + "|" + (d ? d : "");
-}
+}  // namespace
 
+namespace rtrt {
+std::string scene_prep_hooks()
+{
+    std::string h;
+    for (const char *k : {"RT_SPT_NO_BVH", "RT_SPT_GEO", "RT_SPT_WIDE", "RT_SPT_WIDE_LEAF", "RT_WIDE_WPB"}) {
+        const char *v = getenv(k);
+        h += v ? v : "-";
+        h += "|";
+    }
+    return h;
+}
+}  // namespace rtrt
+
+namespace {
 // Caller holds the device state's lock.
 int cached_scene(const rtrt::DeviceState &st, const rt_sphere *spheres, unsigned n, spt_scene **out)
 {
     SceneCache &c = g_scene_cache[st.device];
-    const std::string hooks = prep_hooks();
+    const std::string hooks = rtrt::scene_prep_hooks();
     if (c.sc && c.host.size() == n && c.hooks == hooks &&
         memcmp(c.host.data(), spheres, sizeof(rt_sphere) * n) == 0) {
         *out = c.sc;

@@ -10,11 +10,13 @@
 // never leave its device and a render call needs no exchange at all.  The
 // host-buffer paths (spt_render_multi, spt_multi_download) assemble the frame
 // in the caller's memory band by band.  Only a device-resident frame on every
-// GPU needs a collective: one RCCL group -- ncclGroupStart, one ncclBroadcast
-// rooted at each band (an all-gather of unequal bands), ncclGroupEnd -- over
-// xGMI, after which each device repacks its RGBA8 frame with the kernel's own
-// toInt (spt_pack_pixels_async).  RCCL is loaded on first use (dlopen), so
-// the single-GPU library needs nothing but the HIP runtime.
+// GPU needs a collective: the bands are equal (B = ceil(h/N) rows; the last
+// is shorter, its padding rows past h never read), so one in-place
+// ncclAllGather over xGMI assembles the accumulator on every device, which
+// then repacks its RGBA8 frame with the kernel's own toInt
+// (spt_pack_pixels_async).  RCCL is loaded on first use (dlopen), so the
+// single-GPU library needs nothing but the HIP runtime.
+#include <algorithm>
 #include <dlfcn.h>
 #include <mutex>
 #include <stdlib.h>
@@ -46,7 +48,7 @@ struct Rccl {
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
-    decltype(&ncclBroadcast) broadcast = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
     decltype(&ncclGetErrorString) err = nullptr;
 };
 Rccl g_rccl;
@@ -71,10 +73,10 @@ const Rccl *rccl()
     g_rccl.destroy = (decltype(g_rccl.destroy))dlsym(h, "ncclCommDestroy");
     g_rccl.group_start = (decltype(g_rccl.group_start))dlsym(h, "ncclGroupStart");
     g_rccl.group_end = (decltype(g_rccl.group_end))dlsym(h, "ncclGroupEnd");
-    g_rccl.broadcast = (decltype(g_rccl.broadcast))dlsym(h, "ncclBroadcast");
+    g_rccl.all_gather = (decltype(g_rccl.all_gather))dlsym(h, "ncclAllGather");
     g_rccl.err = (decltype(g_rccl.err))dlsym(h, "ncclGetErrorString");
     g_rccl.ok = g_rccl.init_all && g_rccl.destroy && g_rccl.group_start && g_rccl.group_end &&
-                g_rccl.broadcast && g_rccl.err;
+                g_rccl.all_gather && g_rccl.err;
     if (!g_rccl.ok) snprintf(g_rccl.why, sizeof(g_rccl.why), "librccl lacks an nccl* entry point");
     return &g_rccl;
 }
@@ -90,6 +92,7 @@ int fail_nccl(const Rccl *r, ncclResult_t e, const char *what)
 
 struct spt_multi {
     int w = 0, h = 0;
+    int brows = 0;                     // rows per band (the last band may hold fewer, or none)
     std::vector<Band> bands;
     bool distinct = true;              // no device repeats: RCCL gather possible
     std::vector<ncclComm_t> comms;     // one per band (created on first RCCL gather)
@@ -178,7 +181,9 @@ extern "C" int spt_multi_create(const rt_sphere *spheres, unsigned nspheres, int
     m->w = w;
     m->h = h;
     m->bands.resize(ngpus);
+    m->brows = (h + ngpus - 1) / ngpus;
     const size_t npx = (size_t)w * h;
+    const size_t npad = (size_t)w * m->brows * ngpus;    // colour rows incl. the all-gather's padding
     int rc = RT_OK;
     for (int k = 0; k < ngpus && rc == RT_OK; k++) {
         Band &b = m->bands[k];
@@ -187,19 +192,19 @@ extern "C" int spt_multi_create(const rt_sphere *spheres, unsigned nspheres, int
         for (int j = 0; j < k; j++)
             if (m->bands[j].device == dev) m->distinct = false;
         b.device = dev;
-        b.s0 = (int)((long long)k * h / ngpus);
-        b.s1 = (int)((long long)(k + 1) * h / ngpus);
+        b.s0 = std::min(h, k * m->brows);
+        b.s1 = std::min(h, (k + 1) * m->brows);
         if ((rc = scope.select(dev))) break;
         if ((rc = spt_scene_create(spheres, nspheres, &b.scene))) break;   // checks gfx950 too
         if ((rc = scope.select(dev))) break;
         e = hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&b.rendered, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&b.gathered, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipMalloc(&b.d_col, 3 * sizeof(float) * npx);
+        if (e == hipSuccess) e = hipMalloc(&b.d_col, 3 * sizeof(float) * npad);
         if (e == hipSuccess) e = hipMalloc(&b.d_seed, 2 * sizeof(uint32_t) * npx);
         if (e == hipSuccess) e = hipMalloc(&b.d_px, sizeof(uint32_t) * npx);
         if (e == hipSuccess) e = hipMalloc(&b.d_cnt, 4 * sizeof(unsigned long long));
-        if (e == hipSuccess) e = hipMemsetAsync(b.d_col, 0, 3 * sizeof(float) * npx, b.stream);
+        if (e == hipSuccess) e = hipMemsetAsync(b.d_col, 0, 3 * sizeof(float) * npad, b.stream);
         if (e == hipSuccess) e = hipMemsetAsync(b.d_px, 0, sizeof(uint32_t) * npx, b.stream);
         if (e == hipSuccess) e = hipMemsetAsync(b.d_cnt, 0, 4 * sizeof(unsigned long long), b.stream);
         if (e == hipSuccess) e = hipEventRecord(b.gathered, b.stream);
@@ -301,19 +306,18 @@ extern "C" int spt_multi_gather_async(spt_multi *m)
             ncclResult_t ne = r->init_all(m->comms.data(), n, devs.data());
             if (ne != ncclSuccess) { m->comms.clear(); return fail_nccl(r, ne, "ncclCommInitAll"); }
         }
+        // One in-place all-gather: rank k sends its band (slot rows
+        // [k B, (k+1) B), padded) from where the full buffer holds it.
+        const size_t cnt = 3 * px_off(*m, m->brows);
         ncclResult_t ne = r->group_start();
         if (ne != ncclSuccess) return fail_nccl(r, ne, "ncclGroupStart");
-        for (int root = 0; root < n && ne == ncclSuccess; root++) {
-            const Band &src = m->bands[root];
-            const size_t o = 3 * px_off(*m, src.s0), cnt = 3 * px_off(*m, src.s1) - o;
-            for (int k = 0; k < n && ne == ncclSuccess; k++) {
-                Band &b = m->bands[k];
-                if ((rc = scope.select(b.device))) { (void)r->group_end(); return rc; }
-                ne = r->broadcast(b.d_col + o, b.d_col + o, cnt, ncclFloat32, root, m->comms[k], b.stream);
-            }
+        for (int k = 0; k < n && ne == ncclSuccess; k++) {
+            Band &b = m->bands[k];
+            if ((rc = scope.select(b.device))) { (void)r->group_end(); return rc; }
+            ne = r->all_gather(b.d_col + (size_t)k * cnt, b.d_col, cnt, ncclFloat32, m->comms[k], b.stream);
         }
         ncclResult_t ge = r->group_end();
-        if (ne != ncclSuccess) return fail_nccl(r, ne, "ncclBroadcast");
+        if (ne != ncclSuccess) return fail_nccl(r, ne, "ncclAllGather");
         if (ge != ncclSuccess) return fail_nccl(r, ge, "ncclGroupEnd");
     } else {
         for (Band &b : m->bands) {
@@ -437,11 +441,6 @@ struct MultiCache {
 MultiCache g_multi_cache;
 std::mutex g_multi_mu;
 
-std::string multi_hooks()
-{
-    const char *a = getenv("RT_SPT_NO_BVH"), *b = getenv("RT_SPT_GEO"), *c = getenv("RT_SPT_WIDE");
-    return std::string(a ? "1" : "0") + "|" + (b ? b : "") + "|" + (c ? c : "");
-}
 }  // namespace
 
 namespace rtrt {
@@ -475,7 +474,7 @@ extern "C" int spt_render_multi(const rt_sphere *spheres, unsigned nspheres, con
     MultiCache &c = g_multi_cache;
     std::vector<int> devs(ngpus);
     for (int k = 0; k < ngpus; k++) devs[k] = devices ? devices[k] : k;
-    const std::string hooks = multi_hooks();
+    const std::string hooks = rtrt::scene_prep_hooks();
     int rc = RT_OK;
     if (!(c.m && c.devices == devs && c.w == w && c.h == h)) {
         destroy_multi(c.m);

@@ -1196,7 +1196,12 @@ int render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int 
     int nstream = (long long)w * ngroups * 16 * nsub >= STREAM2_TREES ? 2 : 1;
     if (const char *e = getenv("RT_WHITTED_STREAMS")) nstream = atoi(e) >= 2 ? 2 : 1;
     if (nstream == 2) {
-        nslab = std::min<long long>(std::max<long long>(nslab, 2), ngroups);
+        // Two arenas are live at once: each slab holds at most SLAB_TREES / 2
+        // trees, so both together stay within one single-stream arena (1080p
+        // window: 2 slabs as before; full-height 1080p 3, 3840x2400 10).
+        const long long half_groups = std::max<long long>(1, (SLAB_TREES / 2) / ((long long)w * 16 * nsub));
+        nslab = std::max<long long>(nslab, std::max<long long>(2, (ngroups + half_groups - 1) / half_groups));
+        nslab = std::min<long long>(nslab, ngroups);
         if (nslab < 2) nstream = 1;
     }
     // Two slabs on two streams: the second slab's root kernel can start only
@@ -1230,8 +1235,10 @@ int render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int 
         if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async fork");
     }
     unsigned long long *cnt = (unsigned long long *)d_counters;
+    // (after the fork, an error return still joins the second stream back)
+    const auto bail = [&](int code) { return nstream == 2 ? rtrt::join_aux_on_error(*st, s, code) : code; };
     for (int i = 0; i < nstream; i++) {
-        if ((rc = wavefront_arena(*st, i ? SLOT_WF2 : SLOT_WF, w, slab_rows, nsub, &A[i]))) return rc;
+        if ((rc = wavefront_arena(*st, i ? SLOT_WF2 : SLOT_WF, w, slab_rows, nsub, &A[i]))) return bail(rc);
         A[i].side = side;
         A[i].nsub = nsub;
         A[i].ocl = ocl;
@@ -1250,15 +1257,15 @@ int render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int 
         a.ntrees = a.npix * nsub;
         hipError_t e = hipMemsetAsync(a.count, 0, sizeof(int) * rt::whitted::C_TOTAL * rt::whitted::CSTRIDE, sk);
         if (e == hipSuccess) e = hipMemsetAsync(a.fixbits, 0, sizeof(unsigned) * (((size_t)a.ntrees + 31) / 32), sk);
-        if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async memset");
+        if (e != hipSuccess) return bail(rtrt::fail_hip(e, "rtw_render_async memset"));
         rc = cnt ? launch_wavefront<true>(a, w, srows, row_end, d_sx, d_sy, DX, DY, cnt, sk, d_xrgb)
                  : launch_wavefront<false>(a, w, srows, row_end, d_sx, d_sy, DX, DY, cnt, sk, d_xrgb);
-        if (rc) return rc;
+        if (rc) return bail(rc);
     }
     if (nstream == 2) {
         hipError_t e = hipEventRecord(st->join_ev, st->aux);
         if (e == hipSuccess) e = hipStreamWaitEvent(s, st->join_ev, 0);
-        if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async join");
+        if (e != hipSuccess) return bail(rtrt::fail_hip(e, "rtw_render_async join"));
     }
     hipError_t e = hipEventRecord(st->wf_done, s);
     if (e != hipSuccess) return rtrt::fail_hip(e, "rtw_render_async record");

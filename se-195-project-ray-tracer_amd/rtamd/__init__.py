@@ -19,12 +19,12 @@ import numpy as np
 
 from . import ppm, scenes
 from ._lib import (Camera, Float4, Primitive, QPrimitive, RTError, Sphere, Vec3, check, device_count, lib,
-                   set_device, SPT_DIRECT_LIGHTING, SPT_PATH_TRACING)
+                   set_device, SPT_COUNT_RAYS, SPT_DIRECT_LIGHTING, SPT_PATH_TRACING)
 
 __all__ = ["Camera", "Primitive", "QPrimitive", "Float4", "Sphere", "Vec3", "RTError", "scenes", "lib", "check",
            "device_count", "set_device", "whitted_render", "queue_render", "SmallptFrame", "SmallptScene",
            "SmallptMulti",
-           "SPT_PATH_TRACING", "SPT_DIRECT_LIGHTING"]
+           "SPT_PATH_TRACING", "SPT_DIRECT_LIGHTING", "SPT_COUNT_RAYS"]
 
 
 def whitted_render(w, h, row_begin=20, row_end=None, prims=None, nprims=None, frame=None,
@@ -134,8 +134,8 @@ class SmallptScene:
 class SmallptMulti:
     """A frame tiled in row bands over several devices (spt_multi_*): band k
     renders pixel rows [h - rows[k+1], h - rows[k]) on devices[k]; gather()
-    assembles the whole frame on every band's device (RCCL group of
-    broadcasts, or peer copies when a device repeats)."""
+    assembles the whole frame on every band's device (one RCCL all-gather of
+    the equal padded bands, or peer copies when a device repeats)."""
 
     def __init__(self, w, h, devices, spheres=None, nspheres=None):
         if spheres is None:

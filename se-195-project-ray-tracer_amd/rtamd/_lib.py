@@ -13,12 +13,14 @@ LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(PKG_DIR, "librt_hip.so")
 
 RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NODEVICE = 0, -1, -2, -3
 SPT_PATH_TRACING, SPT_DIRECT_LIGHTING = 0, 1
+SPT_COUNT_RAYS = 0x100
 
 # Every symbol include/rt_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = ("rt_last_error", "rt_device_count", "rt_set_device", "rt_release", "rt_cached_bytes",
            "rt_host_alloc", "rt_host_free",
            "rtw_render", "rtw_render_async", "rtw_render_ocl", "rtw_render_ocl_async", "spt_render", "spt_render_async", "spt_seed_fill",
            "spt_scene_create", "spt_scene_destroy", "spt_scene_render_async", "spt_scene_render_groups_async",
+           "spt_group_count", "spt_scene_render_list_async", "spt_groups_pack_async", "spt_groups_unpack_async",
            "spt_pack_pixels_async",
            "spt_multi_create", "spt_multi_destroy", "spt_multi_set_scene", "spt_multi_bands", "spt_multi_upload",
            "spt_multi_render_async", "spt_multi_gather_async", "spt_multi_sync", "spt_multi_download",
@@ -104,6 +106,11 @@ def lib():
         L.spt_scene_render_groups_async.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, i, u64p, vp]
     if hasattr(L, "spt_pack_pixels_async"):   # (absent from older A/B builds under RT_HIP_LIB)
         L.spt_pack_pixels_async.argtypes = [vp, vp, i, i, i, i, vp]
+    if hasattr(L, "spt_scene_render_list_async"):
+        L.spt_group_count.argtypes = [i, i]
+        L.spt_scene_render_list_async.argtypes = [vp, vp, vp, vp, vp, vp, i, i, vp, i, i, i, i, u64p, vp, vp]
+        L.spt_groups_pack_async.argtypes = [vp, i, i, vp, i, vp, vp]
+        L.spt_groups_unpack_async.argtypes = [vp, i, i, vp, i, vp, vp]
     L.spt_seed_fill.restype = None
     if hasattr(L, "spt_multi_create"):
         ip = C.POINTER(C.c_int)

@@ -31,6 +31,25 @@ if %(mode)r == "bands":
     g = rd.FrameGather(tc, tp, rank, world, w, h)
     g.gather()
     rd.gather_seeds(ts, rank, world, w, h)
+elif %(mode)r == "lists":
+    # cost-balanced group lists (balanced_partition over made-up costs): each
+    # rank keeps only its groups of an oracle frame, then ListGather (host
+    # pack / unpack) must rebuild the whole accumulator on every rank
+    O.smallpt_render(S, n, cam, col, seeds, px, w, h, 0, spp)
+    costs = [(g * 7919) %% 13 + (g %% 5 == 0) * 40 for g in range(rd.group_count(w, h))]
+    parts = rd.balanced_partition(costs, world)
+    keep = np.zeros(w * h, bool)
+    sl = rd.group_slots(parts[rank], w, h)
+    keep[sl[sl >= 0]] = True
+    col.reshape(-1, 3)[~keep] = 0.0
+    g = rd.ListGather(tc, tp, rank, world, w, h, parts, pack=lambda: None)
+    g.gather()
+    c2 = np.zeros_like(col); s2 = O.seeds(w, h); p2 = np.zeros_like(px)
+    O.smallpt_render(S, n, cam, c2, s2, p2, w, h, 0, spp)
+    ok = (col.view(np.uint32) == c2.view(np.uint32)).all() and sorted(sum(parts, [])) == list(range(rd.group_count(w, h)))
+    print("RANK", rank, "OK" if ok else "MISMATCH", flush=True)
+    dist.destroy_process_group()
+    sys.exit(0)
 else:
     for g0 in range(rank, (h + 7) // 8, world):         # this rank's 8-row groups
         O.smallpt_render(S, n, cam, col, seeds, px, w, h, 0, spp, row_begin=8 * g0, row_end=min(8 * g0 + 8, h))
@@ -60,7 +79,8 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("world,mode", [(2, "bands"), (4, "bands"), (2, "groups"), (3, "groups")])
+@pytest.mark.parametrize("world,mode", [(2, "bands"), (4, "bands"), (2, "groups"), (3, "groups"), (2, "lists"),
+                                        (3, "lists")])
 def test_band_gather_is_exact(tmp_path, world, mode):
     script = tmp_path / "w.py"
     script.write_text(WORKER % {"pkg": os.path.join(ROOT, "se-195-project-ray-tracer_amd"),
@@ -94,3 +114,25 @@ def test_row_band_layout():
     assert covered == list(range(1080))
     with pytest.raises(ValueError):
         rd.row_band(0, 7, 1080)
+
+
+def test_balanced_partition_properties():
+    """Every group exactly once; each rank's list in decreasing cost; the
+    heaviest `world` groups on distinct ranks; loads within the largest
+    single cost of each other (the longest-first greedy bound)."""
+    import numpy as np
+    from rtamd import dist as rd
+    rng = np.random.default_rng(3)
+    for world in (1, 2, 3, 8):
+        costs = rng.integers(1, 1000, 8100) * (rng.random(8100) < 0.3) + 1
+        parts = rd.balanced_partition(costs, world)
+        assert sorted(sum(parts, [])) == list(range(8100))
+        for p in parts:
+            assert all(costs[a] >= costs[b] for a, b in zip(p, p[1:]))
+        top = np.argsort(-costs, kind="stable")[:world]
+        owner = {g: r for r, p in enumerate(parts) for g in p}
+        assert len({owner[g] for g in top}) == world
+        loads = [int(costs[p].sum()) for p in parts]
+        assert max(loads) - min(loads) <= costs.max()
+    assert rd.interleaved_groups(1, 4, 1920, 1080)[:3] == [60, 61, 62]
+    assert sum(len(rd.interleaved_groups(k, 3, 197, 61)) for k in range(3)) == rd.group_count(197, 61)

@@ -116,12 +116,15 @@ def test_random_scenes_vs_oracle(rt, oracle, seed):
     assert (got == ref).all() and gc == rc
 
 
+@pytest.mark.parametrize("streams", ["1", "2"])
 @pytest.mark.parametrize("slabs", [2, 3, 7])
-def test_interleaved_slabs_bit_exact(rt, oracle, slabs, monkeypatch):
+def test_interleaved_slabs_bit_exact(rt, oracle, slabs, streams, monkeypatch):
     """The level pass over several interleaved row slabs (what frames above
     SLAB_TREES trees use) gives the same frame and counts; also with queues
-    small enough to send trees to the fixup pass."""
+    small enough to send trees to the fixup pass.  With two streams, slabs
+    alternate between them and slabs 0, 2, ... reuse the first arena."""
     monkeypatch.setenv("RT_WHITTED_SLABS", str(slabs))
+    monkeypatch.setenv("RT_WHITTED_STREAMS", streams)
     w, h = 320, 240
     ref, rc = oracle.whitted_render(w, h, nthreads=8)
     got, gc = rt.whitted_render(w, h, counters=True)
@@ -159,12 +162,15 @@ def test_slab_tree_word_limit(rt, monkeypatch):
     assert (got == ref).all() and gc == rc
 
 
-def test_device_memory_bounded(rt):
-    """The level pass's device arena for a 1920x1080 frame (two slabs of
-    queues at a third of the slab's trees per level) stays near 1.2 GB."""
+@pytest.mark.parametrize("w,h,r0,r1", [(1920, 1080, 20, 1010), (1920, 1080, 20, 1080), (3840, 2400, 20, 2330)])
+def test_device_memory_bounded(rt, w, h, r0, r1):
+    """The level pass's device memory for the reference window of a 1920x1080
+    frame, a full-height one and a 3840x2400 one stays within one
+    single-stream arena's size: with two streams live at once, each slab
+    holds at most SLAB_TREES / 2 trees."""
     rt.lib().rt_release()
-    rt.whitted_render(1920, 1080)
-    assert rt.lib().rt_cached_bytes() < 1.5e9, rt.lib().rt_cached_bytes()
+    rt.whitted_render(w, h, row_begin=r0, row_end=r1)
+    assert rt.lib().rt_cached_bytes() < 1.55e9, rt.lib().rt_cached_bytes()
 
 
 def test_async_frames_on_other_streams_are_ordered(rt, oracle):
