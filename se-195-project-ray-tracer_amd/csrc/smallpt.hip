@@ -148,8 +148,11 @@ __device__ __forceinline__ int query_bf(const G &geo, const ray3 &r, float &t, i
         bad = bad || fabsf(det) < 0x1p-96f;
         const float sd = sqrt_nr(det);
         const float t1 = b - sd, t2 = b + sd;
-        const float d = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
-        const bool take = d < t;
+        // SphereIntersect's distance is t1 if t1 > EPS, else t2 if t2 > EPS,
+        // else a miss: d = t1 > EPS ? t1 : t2, taken iff d > EPS && d < t
+        // (false for NaN) -- one select fewer than materialising the miss.
+        const float d = t1 > EPS ? t1 : t2;
+        const bool take = d > EPS && d < t;
         t = take ? d : t;
         id = take ? i : id;
         if (COUNT) first = (first < 0 && take) ? i : first;
@@ -168,6 +171,9 @@ __device__ __forceinline__ int query_bf(const G &geo, const ray3 &r, float &t, i
 // (ts = maxt on entry; "some update happened" = IntersectP true, the first
 // update = its early-exit index for the test counter).  Each sphere record
 // is loaded once for both rays, and the two dependency chains interleave.
+// Uncounted, the shadow ray only needs "some distance in (EPS, maxt)"
+// (geomfunc.h:94-110 with a fixed maxt): an occluded flag, not a running
+// minimum and index -- three VALU operations fewer per sphere.
 template <bool COUNT, class G>
 __device__ __forceinline__ void query2_bf(const G &geo, const ray3 &r, float &t, int &id, const ray3 &rs, bool sh,
                                           float &ts, int &ids, int &firsts)
@@ -176,7 +182,7 @@ __device__ __forceinline__ void query2_bf(const G &geo, const ray3 &r, float &t,
     int first = -1;
     id = -1;
     ids = -1;
-    bool bad = false;
+    bool bad = false, occ = false;
 #pragma unroll RT_SPT_QUNROLL
     for (int i = geo.count() - 1; i >= 0; i--) {
         const float4 g = geo.at(i);
@@ -187,8 +193,8 @@ __device__ __forceinline__ void query2_bf(const G &geo, const ray3 &r, float &t,
             bad = bad || fabsf(det) < 0x1p-96f;
             const float sd = sqrt_nr(det);
             const float t1 = b - sd, t2 = b + sd;
-            const float d = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
-            const bool take = d < t;
+            const float d = t1 > EPS ? t1 : t2;          // (query_bf: taken iff d > EPS && d < t)
+            const bool take = d > EPS && d < t;
             t = take ? d : t;
             id = take ? i : id;
         }
@@ -199,13 +205,18 @@ __device__ __forceinline__ void query2_bf(const G &geo, const ray3 &r, float &t,
             bad = bad || (sh && fabsf(det) < 0x1p-96f);
             const float sd = sqrt_nr(det);
             const float t1 = b - sd, t2 = b + sd;
-            const float d = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
-            const bool take = d < ts;
-            ts = take ? d : ts;
-            ids = take ? i : ids;
-            if (COUNT) firsts = (firsts < 0 && take) ? i : firsts;
+            const float d = t1 > EPS ? t1 : t2;
+            const bool take = d > EPS && d < ts;
+            if (COUNT) {
+                ts = take ? d : ts;
+                ids = take ? i : ids;
+                firsts = (firsts < 0 && take) ? i : firsts;
+            } else {
+                occ = occ || take;
+            }
         }
     }
+    if (!COUNT) ids = occ ? 0 : -1;
     if (wave_any(bad)) {
         t = t_in;
         id = query<COUNT>(geo, r, t, first);

@@ -81,7 +81,9 @@ def main():
     libs = sorted(os.listdir(base)) if os.path.isdir(base) else []
     if os.environ.get("LIBS"):
         libs = os.environ["LIBS"].split(",")
-    variants = {name: {"RT_HIP_LIB": os.path.join(base, name, "librt_hip.so")} for name in libs}
+    tree = os.path.join(ROOT, "se-195-project-ray-tracer_amd", "librt_hip.so")   # "main": the in-tree build
+    variants = {name: {"RT_HIP_LIB": tree if name == "main" else os.path.join(base, name, "librt_hip.so")}
+                for name in libs}
     if not variants:
         variants = {"tree": {}}
     for _ in range(int(os.environ.get("ROUNDS", "2"))):

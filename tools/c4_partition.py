@@ -13,9 +13,12 @@ after warm-up frames; median of REPS frames.  The N shares rendered into one
 frame must equal the full-frame render bit for bit (checked).
 
     NS=4,8 REPS=5 python tools/c4_partition.py
+    LIBS=a,b ROUNDS=2 QUICK=1 python tools/c4_partition.py   (A/B of build_ab/<lib> builds:
+        one child process per lib and round; QUICK: balanced lists only)
 """
 import ctypes as C
 import os
+import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -67,6 +70,16 @@ def render_groups(sc, k, N, col, sd, px):
 
 
 def main():
+    if os.environ.get("LIBS") and not os.environ.get("C4_CHILD"):
+        for r in range(int(os.environ.get("ROUNDS", "2"))):
+            for lib in os.environ["LIBS"].split(","):
+                path = os.path.join(ROOT, "build_ab", lib, "librt_hip.so") if lib != "main" else \
+                    os.path.join(ROOT, "se-195-project-ray-tracer_amd", "librt_hip.so")
+                print("--- lib %s round %d" % (lib, r), flush=True)
+                subprocess.run([sys.executable, __file__], env=dict(os.environ, RT_HIP_LIB=path, C4_CHILD="1"),
+                               check=True, timeout=600)
+        return
+    quick = os.environ.get("QUICK") == "1"
     sc_full = rtamd.SmallptScene(spheres, n)
     ref = bufs()
     for _ in range(3):
@@ -81,16 +94,17 @@ def main():
         # interleaved (one scene per rank: each learns its own order)
         res = []
         out = bufs()
-        for k in range(N):
+        for k in (range(N) if not quick else []):
             sc = rtamd.SmallptScene(spheres, n)
             for _ in range(3):
                 render_groups(sc, k, N, *out)
             res.append(timed(lambda: render_groups(sc, k, N, *out)))
             sc.close()
-        print("N=%d interleaved: per rank %s ms; max %.2f" % (N, [round(r[0], 2) for r in res],
-                                                               max(r[0] for r in res)), flush=True)
-        ok = torch.equal(out[0].view(torch.int32), ref[0].view(torch.int32)) and torch.equal(out[2], ref[2])
-        print("  assembled == full frame: %s" % ok, flush=True)
+        if not quick:
+            print("N=%d interleaved: per rank %s ms; max %.2f" % (N, [round(r[0], 2) for r in res],
+                                                                   max(r[0] for r in res)), flush=True)
+            ok = torch.equal(out[0].view(torch.int32), ref[0].view(torch.int32)) and torch.equal(out[2], ref[2])
+            print("  assembled == full frame: %s" % ok, flush=True)
         # learning frame: interleaved lists with per-group costs
         cost = torch.zeros(NG, dtype=torch.int32, device=dev)
         sc = rtamd.SmallptScene(spheres, n)
