@@ -46,7 +46,7 @@ FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: peak FP32 vector
 W, H, SPP = 1920, 1080, 64
 
 
-BENCH_KERNEL = "rt::smallpt::render_kernel<false, false, 0, true>"   # the two-query (DUAL) kernel: Cornell has one light
+BENCH_KERNEL = "rt::smallpt::render_kernel<false, false, 0, true, false>"   # the two-query (DUAL) kernel: Cornell has one light
 
 
 def pmc_digest(kernel):

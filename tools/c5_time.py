@@ -35,16 +35,20 @@ if os.environ.get("BAND"):                          # BAND=k/N: row band k of N 
 GROUP = os.environ.get("GROUP")                    # GROUP=k/N: interleaved 8-row groups of rank k of N
 
 
+MODE = rtamd.SPT_COUNT_RAYS if os.environ.get("COUNTED") == "rays" else 0
+
+
 def run(c=None):
     cp = c.data_ptr() if c is not None else None
+    mode = MODE if c is not None else 0
     if GROUP:
         k, N = (int(v) for v in GROUP.split("/"))
         rtamd.check(L.spt_scene_render_groups_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
-                                                    seeds.data_ptr(), px.data_ptr(), W, H, k, N, 0, SPP, 0, cp,
+                                                    seeds.data_ptr(), px.data_ptr(), W, H, k, N, 0, SPP, mode, cp,
                                                     st.cuda_stream))
     else:
         rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
-                                             seeds.data_ptr(), px.data_ptr(), W, H, R0, R1, 0, SPP, 0, cp,
+                                             seeds.data_ptr(), px.data_ptr(), W, H, R0, R1, 0, SPP, mode, cp,
                                              st.cuda_stream))
 
 
@@ -70,7 +74,9 @@ if stats:
     print("  node visits in the first 64 / 256 / 1024 nodes of the ray's octant layout: %.3f %.3f %.3f" % (
         bs[21] / max(bs[0], 1), bs[22] / max(bs[0], 1), bs[23] / max(bs[0], 1)))
 ts = []
-COUNTED = os.environ.get("COUNTED") == "1"          # time the counted kernel instead
+COUNTED = os.environ.get("COUNTED") in ("1", "rays")   # time the counted kernel (full, or rays-only) instead
+for _ in range(int(os.environ.get("WARM", "0"))):      # uncounted frames first (they teach the tile order)
+    run(None)
 for _ in range(int(os.environ.get("REPS", "1"))):
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(st)
@@ -79,8 +85,8 @@ for _ in range(int(os.environ.get("REPS", "1"))):
     torch.cuda.synchronize()
     ts.append(a.elapsed_time(b))
 ms = float(np.median(ts))
-print("c5 %dx%d rows [%d,%d) spp=%d spheres=%d%s: %.2f ms (median of %d, min %.2f), rays %d, %.1f Mrays/s, sphere tests %d" % (
-    W, H, R0, R1, SPP, n, " counted" if COUNTED else "", ms, len(ts), min(ts), rays, rays / ms / 1e3, int(cnt[2])))
+print("c5 %dx%d rows [%d,%d) spp=%d spheres=%d%s%s: %.2f ms (median of %d, min %.2f), rays %d, %.1f Mrays/s, sphere tests %d" % (
+    W, H, R0, R1, SPP, n, " counted" if COUNTED else "", " (rays only)" if MODE else "", ms, len(ts), min(ts), rays, rays / ms / 1e3, int(cnt[2])))
 if int(cnt[7]):
     q = rays
     print("  per query: %.1f nodes, %.1f sphere tests; lane trips / (64 x wave trips) = %.3f" % (
