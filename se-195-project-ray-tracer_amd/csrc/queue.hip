@@ -148,6 +148,19 @@ __device__ __forceinline__ float plane_cand(float4 g, const ray3 &r)
     return cand;
 }
 
+#ifndef RT_Q_LEAN
+#define RT_Q_LEAN 3         // trace()'s loops without per-lane branches: bit 0 spheres, bit 1 planes (A/B: 0)
+#endif
+
+// plane_cand without branches: the division for every lane, its result kept
+// only where the reference divides (d != 0) and t > 0.
+__device__ __forceinline__ float plane_cand_lean(float4 g, const ray3 &r)
+{
+    const float d = g.x * r.d.x + g.y * r.d.y + g.z * r.d.z;
+    const float t = -((g.x * r.o.x + g.y * r.o.y + g.z * r.o.z) + g.w) / d;
+    return (d != 0 && t > 0) ? t : __builtin_inff();
+}
+
 // get_normal, :162-177.
 __device__ __forceinline__ v3 normal_at(const Scene &S, int p, v3 pt)
 {
@@ -171,17 +184,53 @@ __device__ Hit trace(const Scene &S, const ray3 &ray)
     // :181-193 nearest hit below 1e7, lowest index on ties.
     float dist = 10000000.0f;
     int prim = -1, result = 1;
-    for (int k = 0; k < S.ns; k++) {
-        int res;
-        const float c = sphere_cand(S.sph[k], ray, res);
-        const int id = S.sph_id[k];
-        if (res && (c < dist || (c == dist && prim >= 0 && id < prim))) { dist = c; prim = id; result = res; }
+    bool bad = !(RT_Q_LEAN & 1);
+    if (RT_Q_LEAN & 1) {
+        // sphere_cand as one wave-uniform branch over a straight-line body
+        // (sqrt_nr for every lane, its range checked once per loop): the
+        // nested per-lane branches cost more mask instructions than VALU.
+        for (int k = 0; k < S.ns; k++) {
+            const float4 g = S.sph[k];
+            const float vx = ray.o.x - g.x, vy = ray.o.y - g.y, vz = ray.o.z - g.z;
+            float b = vx * ray.d.x + vy * ray.d.y + vz * ray.d.z;
+            b = -b;
+            const float det = (b * b) - (vx * vx + vy * vy + vz * vz) + g.w;
+            if (wave_any(det > 0)) {
+                const float sq = sqrt_nr(det);
+                bad = bad || (det > 0 && !sqrt_nr_ok(det));
+                const float i1 = b - sq, i2 = b + sq;
+                const float c = i1 < 0 ? i2 : i1;
+                const int id = S.sph_id[k];
+                const bool take = det > 0 && i2 > 0 && (c < dist || (c == dist && prim >= 0 && id < prim));
+                dist = take ? c : dist;
+                prim = take ? id : prim;
+                result = take ? (i1 < 0 ? -1 : 1) : result;
+            }
+        }
+    }
+    if (wave_any(bad)) {                                    // (rare: det outside sqrt_nr's range)
+        dist = 10000000.0f;
+        prim = -1;
+        result = 1;
+        for (int k = 0; k < S.ns; k++) {
+            int res;
+            const float c = sphere_cand(S.sph[k], ray, res);
+            const int id = S.sph_id[k];
+            if (res && (c < dist || (c == dist && prim >= 0 && id < prim))) { dist = c; prim = id; result = res; }
+        }
     }
 #pragma unroll 4
     for (int k = 0; k < S.np; k++) {
-        const float c = plane_cand(S.pln[k], ray);
+        const float c = (RT_Q_LEAN & 2) ? plane_cand_lean(S.pln[k], ray) : plane_cand(S.pln[k], ray);
         const int id = S.pln_id[k];
-        if (c < dist || (c == dist && prim >= 0 && id < prim)) { dist = c; prim = id; result = 1; }
+        if (RT_Q_LEAN & 2) {
+            const bool take = c < dist || (c == dist && prim >= 0 && id < prim);
+            dist = take ? c : dist;
+            prim = take ? id : prim;
+            result = take ? 1 : result;
+        } else if (c < dist || (c == dist && prim >= 0 && id < prim)) {
+            dist = c; prim = id; result = 1;
+        }
     }
     h.prim = prim;
     h.result = result;
@@ -225,17 +274,40 @@ __device__ Hit trace(const Scene &S, const ray3 &ray)
                 // the point; the reference stops at the first, so only its
                 // position matters (test counter).
                 int first = 0x7fffffff;
-                for (int k = 0; k < S.nos; k++) {
-                    int res;
-                    const float c = sphere_cand(S.osph[k], r, res);
-                    if (res && c < len) first = min(first, S.osph_pos[k]);
-                    if (!COUNT && !wave_any(first == 0x7fffffff)) break;
+                bool sbad = !(RT_Q_LEAN & 1);
+                if (RT_Q_LEAN & 1) {
+                    for (int k = 0; k < S.nos; k++) {
+                        const float4 g = S.osph[k];
+                        const float vx = r.o.x - g.x, vy = r.o.y - g.y, vz = r.o.z - g.z;
+                        float b = vx * r.d.x + vy * r.d.y + vz * r.d.z;
+                        b = -b;
+                        const float det = (b * b) - (vx * vx + vy * vy + vz * vz) + g.w;
+                        if (wave_any(det > 0)) {
+                            const float sq = sqrt_nr(det);
+                            sbad = sbad || (det > 0 && !sqrt_nr_ok(det));
+                            const float i1 = b - sq, i2 = b + sq;
+                            const float c = i1 < 0 ? i2 : i1;
+                            const bool occ = det > 0 && i2 > 0 && c < len;
+                            first = occ ? min(first, S.osph_pos[k]) : first;
+                            if (!COUNT && !wave_any(first == 0x7fffffff)) break;
+                        }
+                    }
+                }
+                if (wave_any(sbad)) {
+                    first = 0x7fffffff;
+                    for (int k = 0; k < S.nos; k++) {
+                        int res;
+                        const float c = sphere_cand(S.osph[k], r, res);
+                        if (res && c < len) first = min(first, S.osph_pos[k]);
+                        if (!COUNT && !wave_any(first == 0x7fffffff)) break;
+                    }
                 }
 #pragma unroll 4
                 for (int k = 0; k < S.nop; k++) {
                     if (!COUNT && !wave_any(first == 0x7fffffff)) break;
-                    const float c = plane_cand(S.opln[k], r);
-                    if (c < len) first = min(first, S.opln_pos[k]);
+                    const float c = (RT_Q_LEAN & 2) ? plane_cand_lean(S.opln[k], r) : plane_cand(S.opln[k], r);
+                    if (RT_Q_LEAN & 2) first = c < len ? min(first, S.opln_pos[k]) : first;
+                    else if (c < len) first = min(first, S.opln_pos[k]);
                 }
                 if (first != 0x7fffffff) shade = 0.0f;
                 tests += first != 0x7fffffff ? (unsigned)first + 1u : (unsigned)S.nnonlight;
