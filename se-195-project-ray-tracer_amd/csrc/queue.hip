@@ -736,20 +736,21 @@ level_kernel(QArgs A, int L)
 // batches of FOLD whose loads are all in flight together (consecutive nodes
 // of a level do not depend on each other: the walk is latency-bound).
 constexpr int FOLD = 4;
+#ifndef RT_Q_FOLD_ROOTS
+#define RT_Q_FOLD_ROOTS 3   // final_kernel: trees whose root records are read together (A/B: 1)
+#endif
 
 template <bool COUNT, int COLS>
-__device__ __forceinline__ void fold_tree(const QArgs &A, int tree, int (*ring)[COLS], float &ax, float &ay,
-                                          float &az, unsigned long long (&cnt)[4])
+__device__ __forceinline__ void fold_tree_from(const QArgs &A, float4 c0, int2 ch, int (*ring)[COLS], float &ax,
+                                               float &ay, float &az, unsigned long long (&cnt)[4])
 {
     const int t = threadIdx.x;
-    const float4 c0 = A.rcol[tree];
     ax += c0.x; ay += c0.y; az += c0.z;
     const auto count = [&](unsigned cw) {
         cnt[0] += 1; cnt[1] += (cw >> 16) & 0xff; cnt[2] += cw & 0xffff; cnt[3] += cw >> 24;
     };
     if (COUNT) count(__float_as_uint(c0.w));
     int head = 0, tail = 0;
-    const int2 ch = A.rchild[tree];
     if (ch.x >= 0) ring[tail++ & (RING - 1)][t] = ch.x;
     if (ch.y >= 0) ring[tail++ & (RING - 1)][t] = ch.y;
     for (int lvl = 1; head != tail; lvl++) {
@@ -781,6 +782,15 @@ __device__ __forceinline__ void fold_tree(const QArgs &A, int tree, int (*ring)[
     }
 }
 
+// The tree's root record read here (fix_kernel); final_kernel reads several
+// trees' root records together and calls fold_tree_from.
+template <bool COUNT, int COLS>
+__device__ __forceinline__ void fold_tree(const QArgs &A, int tree, int (*ring)[COLS], float &ax, float &ay,
+                                          float &az, unsigned long long (&cnt)[4])
+{
+    fold_tree_from<COUNT, COLS>(A, A.rcol[tree], A.rchild[tree], ring, ax, ay, az, cnt);
+}
+
 // :436-447: (int) as x86 converts (an overflowing or NaN sum packs 0), 255
 // clamp, uchar_4 (r, g, b, 0).
 __device__ __forceinline__ uint32_t pack_pixel(float ax, float ay, float az)
@@ -808,8 +818,27 @@ final_kernel(QArgs A, int row_end, uint32_t *__restrict__ out, unsigned long lon
     if (x < A.w && y < row_end && !pix_flagged(A, pix)) {
         const float4 ps = A.psum[pix];
         float ax = ps.x, ay = ps.y, az = ps.z;
+#if RT_Q_FOLD_ROOTS > 1
+        // The root records of RT_Q_FOLD_ROOTS trees loaded together (one
+        // latency instead of one per tree), then each tree folded in order.
+        constexpr int T = RT_Q_FOLD_ROOTS;
+        for (int s0 = __float_as_int(ps.w); s0 < NSUB; s0 += T) {
+            float4 c0[T];
+            int2 ch[T];
+#pragma unroll
+            for (int j = 0; j < T; j++) {
+                const int tree = (s0 + j < NSUB ? s0 + j : s0) * A.npix + pix;
+                c0[j] = A.rcol[tree];
+                ch[j] = A.rchild[tree];
+            }
+#pragma unroll
+            for (int j = 0; j < T; j++)
+                if (s0 + j < NSUB) fold_tree_from<COUNT, 256>(A, c0[j], ch[j], ring, ax, ay, az, cnt);
+        }
+#else
         for (int sub = __float_as_int(ps.w); sub < NSUB; sub++)
             fold_tree<COUNT, 256>(A, sub * A.npix + pix, ring, ax, ay, az, cnt);
+#endif
         out[(size_t)y * A.w + x] = pack_pixel(ax, ay, az);
     }
     if (COUNT) flush_counters<4>(counters, cnt);
