@@ -737,7 +737,7 @@ level_kernel(QArgs A, int L)
 // of a level do not depend on each other: the walk is latency-bound).
 constexpr int FOLD = 4;
 #ifndef RT_Q_FOLD_ROOTS
-#define RT_Q_FOLD_ROOTS 3   // final_kernel: trees whose root records are read together (A/B: 1)
+#define RT_Q_FOLD_ROOTS 9   // final_kernel: trees whose root records are read together (all nine; A/B: 1, 3, 5)
 #endif
 
 template <bool COUNT, int COLS>
