@@ -150,3 +150,21 @@ def test_bad_arguments(rt):
     assert rt.lib().rtq_render(C.addressof(P), 65, px.ctypes.data, 4, 4, None) == rt._lib.RT_ERR_INVALID
     assert rt.lib().rtq_render_async(C.addressof(P), n, px.ctypes.data, 4, 4, 3, 2, None, None) == \
         rt._lib.RT_ERR_INVALID
+
+
+def test_sphere_loop_exact_redo(rt):
+    """The queue tracer's lean sphere loops (queue.hip RT_Q_LEAN) redo a loop
+    exactly when a discriminant leaves sqrt_nr's range: a sphere of infinite
+    radius (never hit) forces that redo in every loop; frame and counters stay
+    the oracle's."""
+    P, n = O.queue_scene()
+    p = P[n]
+    p.type = 1
+    p.center = O.F4(1.0, -2.0, 25.0, 0.0)
+    p.radius, p.sq_radius, p.r_radius = float("inf"), float("inf"), 0.0
+    p.m_color = O.F4(0.5, 0.5, 0.5, 0.0)
+    p.m_diff, p.m_spec = 1.0, 0.0
+    ref, rc = O.queue_render(160, 120, P, n + 1, nthreads=NT)
+    px, cnt = rt.queue_render(160, 120, P, n + 1, counters=True)
+    assert (px == ref).all()
+    assert cnt == rc

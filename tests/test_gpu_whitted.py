@@ -211,3 +211,23 @@ def test_pool_grows_after_overflow(rt, oracle, monkeypatch):
         assert (got == ref).all() and gc == rc
         sizes.append(rt.lib().rt_cached_bytes())
     assert sizes[-1] > sizes[0], sizes
+
+
+def test_sphere_loop_exact_redo(rt, oracle):
+    """trace()'s sphere loops use sqrt_nr for every lane and redo the whole
+    loop with the exact per-sphere test when some lane's discriminant is
+    outside its range (whitted.hip RT_WH_LEAN).  A non-light sphere of
+    infinite radius makes every discriminant +inf -- never a hit, but a redo
+    in every nearest and occluder loop: frame and counters stay the
+    oracle's."""
+    from rtamd.scenes import SPHERE, _prim, whitted_scene
+    S, n = whitted_scene()
+    P = (rt.Primitive * (n + 2))()
+    for i in range(n):
+        P[i] = S[i]
+    _prim(P[n], SPHERE, 1.0, -2.0, 25.0, float("inf"), 0.5, 0.5, 0.5, 0.0, 0.0, 1.0, 1.0, 0.0, False)
+    _prim(P[n + 1], SPHERE, -1.0, 1.0, 20.0, 1e-15, 0.5, 0.5, 0.5, 0.3, 0.0, 1.0, 1.0, 0.5, False)
+    w, h = 200, 150
+    ref, rc = oracle.whitted_render(w, h, nthreads=8, prims=P, n=n + 2)
+    got, gc = rt.whitted_render(w, h, prims=P, nprims=n + 2, counters=True)
+    assert (got == ref).all() and gc == rc
