@@ -161,6 +161,8 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
         // sphere_cand as one wave-uniform branch over a straight-line body
         // (sqrt_nr for every lane, its range checked once per loop): the
         // nested per-lane branches cost more mask instructions than VALU.
+        // det <= 0 or NaN needs no test of its own: sqrt_nr returns NaN
+        // there (v_rsq of a negative, 0 x inf at zero), so i2 > 0 fails.
         for (int k = 0; k < S.ns; k++) {
             const float4 g = S.sph[k];
             const float vx = ray.o.x - g.x, vy = ray.o.y - g.y, vz = ray.o.z - g.z;
@@ -173,7 +175,7 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
                 const float i1 = b - sd, i2 = b + sd;
                 const float c = i1 < 0 ? i2 : i1;
                 const int id = S.sph_id[k];
-                const bool take = det > 0 && i2 > 0 && (c < dist || (c == dist && id < prim));
+                const bool take = i2 > 0 && (c < dist || (c == dist && id < prim));
                 dist = take ? c : dist;
                 prim = take ? id : prim;
                 result = take ? (i1 < 0 ? -1 : 1) : result;
@@ -271,7 +273,7 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
                         sbad = sbad || (det > 0 && !sqrt_nr_ok(det));
                         const float i1 = b - sd, i2 = b + sd;
                         const float c = i1 < 0 ? i2 : i1;
-                        const bool occ = det > 0 && i2 > 0 && c < tdist;
+                        const bool occ = i2 > 0 && c < tdist;
                         first = occ ? min(first, S.osph_pos[k]) : first;
                         if (!COUNT && !wave_any(first == 0x7fffffff)) break;
                     }
