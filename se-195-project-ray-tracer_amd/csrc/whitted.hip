@@ -84,6 +84,9 @@ __device__ __forceinline__ float sphere_cand(float4 g, const ray3 &r, int &res)
     return cand;
 }
 
+#ifndef RT_PLANE_ONECHECK
+#define RT_PLANE_ONECHECK 1   // occluder planes: one all-occluded check before the loop, not per plane (A/B: 0)
+#endif
 #ifndef RT_WH_LEAN
 #define RT_WH_LEAN 3        // trace()'s loops without per-lane branches: bit 0 spheres, bit 1 planes (A/B: 0)
 #endif
@@ -288,9 +291,10 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
                     if (!COUNT && !wave_any(first == 0x7fffffff)) break;
                 }
             }
+            const bool pl_any = COUNT || wave_any(first == 0x7fffffff);   // (all occluded by a sphere: no plane test)
 #pragma unroll 4
-            for (int k = 0; k < S.nop; k++) {
-                if (!COUNT && !wave_any(first == 0x7fffffff)) break;
+            for (int k = 0; pl_any && k < S.nop; k++) {
+                if (!COUNT && !RT_PLANE_ONECHECK && !wave_any(first == 0x7fffffff)) break;
                 const float c = (RT_WH_LEAN & 2) ? plane_cand_lean(S.opln[k], r) : plane_cand(S.opln[k], r);
                 if (RT_WH_LEAN & 2) first = c < tdist ? min(first, S.opln_pos[k]) : first;
                 else if (c < tdist) first = min(first, S.opln_pos[k]);
