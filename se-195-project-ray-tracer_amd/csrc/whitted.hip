@@ -84,6 +84,9 @@ __device__ __forceinline__ float sphere_cand(float4 g, const ray3 &r, int &res)
     return cand;
 }
 
+#ifndef RT_SPHERE_EXIT
+#define RT_SPHERE_EXIT 0      // occluder spheres: all-occluded exit after each sphere some lane may hit (A/B: 1; off measured faster)
+#endif
 #ifndef RT_PLANE_ONECHECK
 #define RT_PLANE_ONECHECK 1   // occluder planes: one all-occluded check before the loop, not per plane (A/B: 0)
 #endif
@@ -278,7 +281,7 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
                         const float c = i1 < 0 ? i2 : i1;
                         const bool occ = i2 > 0 && c < tdist;
                         first = occ ? min(first, S.osph_pos[k]) : first;
-                        if (!COUNT && !wave_any(first == 0x7fffffff)) break;
+                        if (!COUNT && RT_SPHERE_EXIT && !wave_any(first == 0x7fffffff)) break;
                     }
                 }
             }
