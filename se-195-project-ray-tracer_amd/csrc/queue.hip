@@ -744,7 +744,10 @@ level_kernel(QArgs A, int L)
 // RING-entry column of pool slots) holds the current level's slots, read in
 // batches of FOLD whose loads are all in flight together (consecutive nodes
 // of a level do not depend on each other: the walk is latency-bound).
-constexpr int FOLD = 4;
+#ifndef RT_Q_FOLD
+#define RT_Q_FOLD 8         // records per batch of the fold's breadth-first walk (A/B: 2,4,6,8,12,16 -> 8 best)
+#endif
+constexpr int FOLD = RT_Q_FOLD;
 #ifndef RT_Q_FOLD_ROOTS
 #define RT_Q_FOLD_ROOTS 9   // final_kernel: trees whose root records are read together (all nine; A/B: 1, 3, 5)
 #endif
