@@ -375,15 +375,27 @@ __device__ __forceinline__ ray3 primary(int sub, float SX, float SY, float DX, f
     return r;
 }
 
-// Builds the SoA scene image from the reference's 96-byte AoS primitives
-// (one block; scene_kernel writes it to the frame's arena once per render).
+// Builds the SoA scene image from the reference's 96-byte AoS primitives:
+// one wave, a lane per primitive (MAXP = 64); each list position is the
+// count of the earlier primitives of its kind (ballot prefix), so the lists
+// keep the reference's order.
 __device__ void build_scene(Scene &S, const rt_primitive *__restrict__ prims, int nprims)
 {
-    for (int p = threadIdx.x; p < nprims; p += blockDim.x) {
-        const rt_primitive &q = prims[p];
-        const bool sph = q.type == SPHERE;
-        S.geo[p] = sph ? make_float4(q.m_Centre.x, q.m_Centre.y, q.m_Centre.z, q.m_SqRadius)
-                       : make_float4(q.plane_N.x, q.plane_N.y, q.plane_N.z, q.plane_D);
+    static_assert(MAXP <= 64, "one lane per primitive");
+    const int p = __lane_id();
+    const bool v = p < nprims;
+    rt_primitive q{};
+    if (v) q = prims[p];
+    const bool light = v && q.m_Light > 0, occluder = v && q.m_Light == 0;
+    const bool sph = v && q.type == SPHERE, pln = v && q.type == PLANE;
+    const unsigned long long below = (1ull << p) - 1ull;       // lanes before this one
+    const auto rank = [&](bool b) { return __popcll(__builtin_amdgcn_ballot_w64(b) & below); };
+    const auto total = [](bool b) { return __popcll(__builtin_amdgcn_ballot_w64(b)); };
+    const int il = rank(light), in = rank(occluder), is = rank(sph), ip = rank(pln);
+    const int ios = rank(sph && occluder), iop = rank(pln && occluder);
+    if (v) {
+        S.geo[p] = q.type == SPHERE ? make_float4(q.m_Centre.x, q.m_Centre.y, q.m_Centre.z, q.m_SqRadius)
+                                    : make_float4(q.plane_N.x, q.plane_N.y, q.plane_N.z, q.plane_D);
         S.mat0[p] = make_float4(q.m_Color.x, q.m_Color.y, q.m_Color.z, q.m_Refl);
         S.mat1[p] = make_float4(q.m_Refr, q.m_Diff, q.m_Spec, q.m_RIndex);
         S.cen[p] = make_float4(q.m_Centre.x, q.m_Centre.y, q.m_Centre.z, 0.f);
@@ -391,32 +403,40 @@ __device__ void build_scene(Scene &S, const rt_primitive *__restrict__ prims, in
         S.type[p] = q.type;
         S.light[p] = q.m_Light;
     }
-    if (threadIdx.x == 0) {
-        int nl = 0, nn = 0, ns = 0, np = 0, nos = 0, nop = 0;
-        for (int p = 0; p < nprims; p++) {
-            const rt_primitive &q = prims[p];
-            const bool occluder = q.m_Light == 0;
-            if (q.m_Light > 0) S.lights[nl++] = p;
-            if (q.type == SPHERE) {
-                S.sph[ns] = make_float4(q.m_Centre.x, q.m_Centre.y, q.m_Centre.z, q.m_SqRadius);
-                S.sph_id[ns++] = p;
-                if (occluder) { S.osph[nos] = S.sph[ns - 1]; S.osph_pos[nos++] = nn; }
-            } else if (q.type == PLANE) {
-                S.pln[np] = make_float4(q.plane_N.x, q.plane_N.y, q.plane_N.z, q.plane_D);
-                S.pln_id[np++] = p;
-                if (occluder) { S.opln[nop] = S.pln[np - 1]; S.opln_pos[nop++] = nn; }
-            }
-            if (occluder) nn++;
-        }
+    if (light) S.lights[il] = p;
+    if (sph) {
+        const float4 g = make_float4(q.m_Centre.x, q.m_Centre.y, q.m_Centre.z, q.m_SqRadius);
+        S.sph[is] = g;
+        S.sph_id[is] = p;
+        if (occluder) { S.osph[ios] = g; S.osph_pos[ios] = in; }
+    } else if (pln) {
+        const float4 g = make_float4(q.plane_N.x, q.plane_N.y, q.plane_N.z, q.plane_D);
+        S.pln[ip] = g;
+        S.pln_id[ip] = p;
+        if (occluder) { S.opln[iop] = g; S.opln_pos[iop] = in; }
+    }
+    const int nl = total(light), nn = total(occluder), ns = total(sph), np = total(pln);
+    const int nos = total(sph && occluder), nop = total(pln && occluder);
+    if (p == 0) {
         S.n = nprims; S.nlights = nl; S.nnonlight = nn;
         S.ns = ns; S.np = np; S.nos = nos; S.nop = nop;
     }
 }
 
-__global__ void __launch_bounds__(64) scene_kernel(const rt_primitive *__restrict__ prims, int nprims,
-                                                   Scene *__restrict__ out)
+// A slab's preparation in one launch: its counters and tree flag words
+// zeroed (grid-stride, 16-B stores) and, when `prims` is given, the arena's
+// scene image built by the first wave (replaces a one-lane scene pass and
+// two fills).
+__global__ void __launch_bounds__(256) prep_kernel(const rt_primitive *__restrict__ prims, int nprims,
+                                                   Scene *__restrict__ scene, uint4 *__restrict__ z0, int n0,
+                                                   uint4 *__restrict__ z1, int n1)
 {
-    build_scene(*out, prims, nprims);
+    if (prims && blockIdx.x == 0 && threadIdx.x < 64) build_scene(*scene, prims, nprims);
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
+        if (i < n0) z0[i] = zero;
+        else z1[i - n0] = zero;
+    }
 }
 
 // Block-cooperative copy of the scene image into LDS (coalesced 16-B loads).
@@ -1325,8 +1345,6 @@ int render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int 
         A[i].ocl = ocl;
         A[i].row_stride = unequal ? period : (int)nslab;
         A[i].row_count = unequal ? (i == 0 ? sp_p : sp_q) : 1;
-        hipLaunchKernelGGL(rt::whitted::scene_kernel, dim3(1), dim3(64), 0, ss[i], d_prims, nprims,
-                           (rt::whitted::Scene *)A[i].scene);
     }
     for (int k = 0; k < (int)nslab; k++) {
         rt::whitted::WfArgs &a = A[k % nstream];
@@ -1336,9 +1354,14 @@ int render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int 
         a.row_begin = row_begin + 16 * (unequal && k == 1 ? sp_p : k);
         a.npix = w * srows;
         a.ntrees = a.npix * nsub;
-        hipError_t e = hipMemsetAsync(a.count, 0, sizeof(int) * rt::whitted::C_TOTAL * rt::whitted::CSTRIDE, sk);
-        if (e == hipSuccess) e = hipMemsetAsync(a.fixbits, 0, sizeof(unsigned) * (((size_t)a.ntrees + 31) / 32), sk);
-        if (e != hipSuccess) return bail(rtrt::fail_hip(e, "rtw_render_async memset"));
+        // counters and tree flag words zeroed; the arena's scene image built by
+        // its first slab (16-B words: the arena rounds every part to 256 B)
+        const auto words = [](size_t bytes) { return (int)((bytes + 15) / 16); };
+        const int nz0 = words(sizeof(int) * rt::whitted::C_TOTAL * rt::whitted::CSTRIDE);
+        const int nz1 = words(sizeof(unsigned) * (((size_t)a.ntrees + 31) / 32));
+        const int pblocks = std::min(1024, std::max(1, (nz0 + nz1 + 255) / 256));
+        hipLaunchKernelGGL(rt::whitted::prep_kernel, dim3(pblocks), dim3(256), 0, sk, k < nstream ? d_prims : nullptr,
+                           nprims, (rt::whitted::Scene *)a.scene, (uint4 *)a.count, nz0, (uint4 *)a.fixbits, nz1);
         rc = cnt ? launch_wavefront<true>(a, w, srows, row_end, d_sx, d_sy, DX, DY, cnt, sk, d_xrgb)
                  : launch_wavefront<false>(a, w, srows, row_end, d_sx, d_sy, DX, DY, cnt, sk, d_xrgb);
         if (rc) return bail(rc);
