@@ -1,0 +1,4 @@
+cd $GRAFT_REPO_ROOT
+for b in 0 1024 1536 2560 3072 4096; do
+  echo "--- blocks=$b"; RT_QUEUE_LEVEL_BLOCKS=$b timeout -k 10 100 python -u tools/queue_time.py 20 2>&1 | grep ms
+done
