@@ -665,7 +665,7 @@ __device__ __forceinline__ int2 queue_children(const QArgs &A, const Scene &S, i
 #define RT_Q_ROOT_MINWAVES 8
 #endif
 #ifndef RT_Q_LEVEL_MINWAVES
-#define RT_Q_LEVEL_MINWAVES 8
+#define RT_Q_LEVEL_MINWAVES 7     // 7: 72 VGPRs, no scratch (8: 64 VGPRs + 28 B/lane scratch since the lean loops); A/B 8/7/6
 #endif
 
 // Level 0: the nine primary rays of every pixel of the slab.
