@@ -53,6 +53,21 @@ def test_random_scenes(rt, seed):
     assert (rt.queue_render(96, 72, P, n) == ref).all()
 
 
+def test_max_primitives(rt):
+    """MAXP = 64 primitives (the scene image is built a lane per primitive,
+    list positions by ballot prefix): lights, spheres and planes shuffled."""
+    rng = np.random.default_rng(77)
+    while True:
+        P, n = O.queue_random_scene(rng, nspheres=52, nlights=4, nplanes_extra=2)
+        ref, rc = O.queue_render(64, 48, P, n, nthreads=NT)
+        if rc[3] == 0:
+            break
+    assert n == 64
+    px, cnt = rt.queue_render(64, 48, P, n, counters=True)
+    assert (px == ref).all()
+    assert cnt == rc
+
+
 def test_undefined_behaviour_is_counted_and_defined(rt):
     """An open scene (rays escape): the reference reads primitives[-1]; both
     the oracle and the library define it as 'no children' and count it."""
