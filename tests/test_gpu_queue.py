@@ -68,6 +68,16 @@ def test_max_primitives(rt):
     assert cnt == rc
 
 
+def test_single_primitive_scene(rt):
+    """One primitive, the reference scene's first wall (open scene: the
+    primitives[-1] read is defined and counted identically)."""
+    P, n = O.queue_scene()
+    ref, rc = O.queue_render(80, 60, P, 1, nthreads=NT)
+    px, cnt = rt.queue_render(80, 60, P, 1, counters=True)
+    assert (px == ref).all()
+    assert cnt == rc
+
+
 def test_undefined_behaviour_is_counted_and_defined(rt):
     """An open scene (rays escape): the reference reads primitives[-1]; both
     the oracle and the library define it as 'no children' and count it."""

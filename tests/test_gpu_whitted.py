@@ -231,3 +231,15 @@ def test_sphere_loop_exact_redo(rt, oracle):
     ref, rc = oracle.whitted_render(w, h, nthreads=8, prims=P, n=n + 2)
     got, gc = rt.whitted_render(w, h, prims=P, nprims=n + 2, counters=True)
     assert (got == ref).all() and gc == rc
+
+
+@pytest.mark.parametrize("light", [False, True])
+def test_single_primitive_scene(rt, oracle, light):
+    """One primitive (the scene image's lists then hold one or no entry: a
+    light sphere has no occluders, a plain one no lights)."""
+    from rtamd.scenes import SPHERE, _prim
+    P = (rt.Primitive * 1)()
+    _prim(P[0], SPHERE, 0.5, 0.0, 12.0, 2.0, 0.7, 0.6, 0.5, 0.4, 0.0, 1.0, 0.8, 0.6, light)
+    ref, rc = oracle.whitted_render(96, 128, nthreads=8, prims=P, n=1)
+    got, gc = rt.whitted_render(96, 128, prims=P, nprims=1, counters=True)
+    assert (got == ref).all() and gc == rc
