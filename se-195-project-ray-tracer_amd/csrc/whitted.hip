@@ -881,6 +881,9 @@ backacc_kernel(WfArgs A, int L)
 // Level 0 of the pixel's nine trees, folded with the FD levels below it
 // (level FD's colours final), the sum over sub-samples (:513-515) and the
 // x28 / clamp / XRGB pack (:517-523).
+#ifndef RT_WH_FINAL_BATCH
+#define RT_WH_FINAL_BATCH 1     // 1: the nine root records read in one round (final_kernel<1> 39.6 -> 33.6 us); 0: a round per tree
+#endif
 template <int FD>
 __global__ void __launch_bounds__(256)
 final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
@@ -895,6 +898,40 @@ final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
     const int pix = r * A.w + x;
     const float4 ps = A.psum[pix];                          // the leading childless trees, summed by root_kernel
     float tr = ps.x, tg = ps.y, tb = ps.z;
+#if RT_WH_FINAL_BATCH
+    // The root records of all the pixel's remaining trees read in one round
+    // (they do not depend on each other), then each tree's children and its
+    // share of the sum in sub-sample order.
+    constexpr int T = 9;                                   // nsub <= 9 (3 x 3; 2 x 2 for openCLcode.cl)
+    const int kf = __float_as_int(ps.w);
+    float4 c0[T];
+    int2 ch[T];
+    int info[T];
+    bool fl[T];
+#pragma unroll
+    for (int j = 0; j < T; j++) {
+        const int sub = kf + j < A.nsub ? kf + j : kf;
+        const int tree = sub * A.npix + pix;
+        if (kf + j < A.nsub) {
+            c0[j] = A.rcol[tree];
+            ch[j] = A.rchild[tree];
+            info[j] = A.rinfo[tree];
+            fl[j] = flagged(A, tree);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < T; j++) {
+        if (kf + j >= A.nsub) continue;
+        float4 c = c0[j];
+        if (!fl[j] && (ch[j].x >= 0 || ch[j].y >= 0)) {
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 cx = ch[j].x >= 0 ? folded<FD - 1>(A, S, ch[j].x) : z;
+            const float4 cy = ch[j].y >= 0 ? folded<FD - 1>(A, S, ch[j].y) : z;
+            c = accumulate(S, c, info[j], ch[j], cx, cy, A.ocl);
+        }
+        tr += c.x; tg += c.y; tb += c.z;
+    }
+#else
     for (int sub = __float_as_int(ps.w); sub < A.nsub; sub++) {
         const int tree = sub * A.npix + pix;
         float4 c0 = A.rcol[tree];
@@ -909,6 +946,7 @@ final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
         }
         tr += c0.x; tg += c0.y; tb += c0.z;
     }
+#endif
     const float scale = A.ocl ? 64.0f : 28.0f;            // 256/4 (openCLcode.cl:238) or 256/9 (:517)
     int red = cvt_i32_x86(tr * scale), green = cvt_i32_x86(tg * scale), blue = cvt_i32_x86(tb * scale);
     if (red > 255) red = 255;
