@@ -508,7 +508,7 @@ constexpr int C_TOTAL = C_SEG + LEVELS * NSEG;
 #define CNT(A, i) ((A).count[(i) * CSTRIDE])
 
 struct WfArgs {
-    const Scene *scene;       // scene image (scene_kernel)
+    const Scene *scene;       // scene image (prep_kernel, the arena's first slab)
     float4 *rcol;             // [ntrees] root colour.xyz, dist
     int *rinfo;               // [ntrees] hit primitive | INFO_*
     float4 *psum;             // [npix] sum (xyz) of the colours of the pixel's leading childless trees,

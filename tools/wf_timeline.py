@@ -9,8 +9,8 @@ import sys
 
 f = glob.glob("%s/**/w_kernel_trace.csv" % sys.argv[1], recursive=True)[0]
 rows = [r for r in csv.DictReader(open(f)) if "whitted" in r["Kernel_Name"]]
-# the last frame: from the second-to-last pair of scene_kernels (two streams) on
-sk = [j for j, r in enumerate(rows) if "scene_kernel" in r["Kernel_Name"]]
+# the last frame: from the second-to-last pair of prep_kernels (two streams) on
+sk = [j for j, r in enumerate(rows) if "prep_kernel" in r["Kernel_Name"]]
 nstreams = 2 if len(sk) >= 2 and int(rows[sk[-1]]["Start_Timestamp"]) - int(rows[sk[-2]]["Start_Timestamp"]) < 50000 else 1
 fr = rows[sk[-nstreams]:]
 t0 = min(int(r["Start_Timestamp"]) for r in fr)
