@@ -743,6 +743,30 @@ def main():
         elapsed, kern_ms = t.tolist()
     ms_per_step = elapsed * 1e3 / args.steps
 
+    # The reference's frame ends in a blocking read of the pixels
+    # (smallptGPU.cpp:760 ReadKernelBuffer after every pass): the same steps
+    # again, each followed by a blocking D2H of the (assembled) RGBA8 frame
+    # into page-locked host memory.  Reported beside ms_per_step (which keeps
+    # the device-resident frame the driver's metric times).
+    host_px = torch.empty(W * H, dtype=torch.int32, pin_memory=True)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        torch.cuda.synchronize(dev)                  # render (+ gather and repack on gs)
+        host_px.copy_(pixels[(nframe[0] - 1) % nbuf], non_blocking=True)
+        torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    rb = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([rb], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        rb = t.item()
+    ms_readback = rb * 1e3 / args.steps
+
     # Roofline: algorithmic HBM bytes of one launch =
     # 32 B per pixel of the band (seeds 8 in + 8 out, colour 12 out, pixel 4
     # out) + the scene (44 B per sphere).  The kernel is VALU-bound; the FP32
@@ -770,6 +794,10 @@ def main():
                        "interleaved 8-row groups" if interleaved else "row bands", world, collective_name(),
                        " (pipelined)" if pipelined else "")) if world > 1 else "single GPU"},
         "frames_per_s": round(1e3 / ms_per_step, 3),
+        "ms_per_frame_with_readback": round(ms_readback, 3),
+        "readback_note": "the same step followed by a blocking D2H of the %dx%d RGBA8 frame (%.1f MB) into "
+                         "pinned host memory, as smallptGPU.cpp:760 reads after every pass; max over ranks" % (
+                             W, H, W * H * 4 / 1e6),
         "Msamples_per_s": round(W * H * SPP / (ms_per_step * 1e-3) / 1e6, 2),
         "rays_per_frame": rays_per_frame,
         "kernel_ms": round(kern_ms, 4),

@@ -183,11 +183,21 @@ int spt_scene_destroy(spt_scene *scene);
  * (one small upload).  Scheduling only -- results are identical; during
  * stream capture the learnt order is used but not updated.  A scene's order
  * is updated by the calling thread: render one scene from one host thread
- * at a time. */
+ * at a time.  Hierarchy scenes give every launch one of 64 work-counter
+ * entries; a launch captured into a graph keeps its entry for the graph's
+ * life (the graph may be replayed at any time), so at most 64 captured
+ * launches of one scene can exist -- the next capture fails RT_ERR_INVALID
+ * until spt_scene_release_captures. */
 int spt_scene_render_async(const spt_scene *scene, const rt_camera *camera, float *d_colors,
                            const uint32_t *d_seeds_in, uint32_t *d_seeds_out, uint32_t *d_pixels,
                            int w, int h, int row_begin, int row_end, int first_sample, int nsamples,
                            int mode, uint64_t *d_counters, void *stream);
+
+/* Hands the work-counter entries held by captured launches of `scene` out
+ * again.  Call it only once every graph captured from this scene's launches
+ * has been destroyed (a replay after it could share an entry with a new
+ * launch). */
+int spt_scene_release_captures(const spt_scene *scene);
 
 /* spt_scene_render_async over an interleaved window: every pixel row y with
  * (y / 8) % ngroups == group, i.e. 8-row groups group, group + ngroups, ...
@@ -207,9 +217,10 @@ int spt_scene_render_groups_async(const spt_scene *scene, const rt_camera *camer
 int spt_group_count(int w, int h);
 
 /* spt_scene_render_async over an explicit set of tile groups: d_groups
- * (device, ngroups DISTINCT entries in [0, spt_group_count(w, h)); entries
- * outside are skipped) in dispatch order -- the first ones start first, so
- * list the costliest first.  A multi-GPU frame split by per-rank lists
+ * (device, ngroups entries in [0, spt_group_count(w, h)); entries outside
+ * are skipped; the list is taken as a set -- a repeated group renders once,
+ * at the dispatch slot of one of its copies) in dispatch order -- the first
+ * ones start first, so list the costliest first.  A multi-GPU frame split by per-rank lists
  * balanced on measured costs (rtamd.dist.balanced_partition).  d_group_cost
  * (nullable, device, spt_group_count(w, h) words; hierarchy scenes only,
  * left unchanged otherwise): each listed group's wave time in 100 MHz ticks

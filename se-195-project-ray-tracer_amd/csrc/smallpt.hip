@@ -2017,6 +2017,27 @@ __global__ void __launch_bounds__(256) groups_copy_kernel(float *__restrict__ co
     }
 }
 
+// A caller's group list made a set (spt_scene_render_list_async): one entry
+// per listed group survives into `out` -- the one whose claim on the group's
+// bit of `claimed` (zeroed) came first -- and every repeat or out-of-range
+// entry becomes -1, which render_kernel skips.  Two waves can then never
+// render the same pixels (their accumulator and seed slots) in one launch, and
+// a group's wave time is added to its cost entry once.  Which copy of a repeat
+// survives moves only its dispatch slot, never a result.
+__global__ void __launch_bounds__(256) list_dedup_kernel(const int *__restrict__ groups, int n, int total,
+                                                         unsigned *__restrict__ claimed, int *__restrict__ out)
+{
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const int g = groups[k];
+        int v = -1;
+        if ((unsigned)g < (unsigned)total) {
+            const unsigned bit = 1u << (g & 31);
+            if (!(atomicOr(&claimed[g >> 5], bit) & bit)) v = g;
+        }
+        out[k] = v;
+    }
+}
+
 }  // namespace smallpt
 }  // namespace rt
 
@@ -2026,6 +2047,7 @@ __global__ void __launch_bounds__(256) groups_copy_kernel(float *__restrict__ co
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <vector>
 #include "rt_runtime.h"
@@ -2072,8 +2094,12 @@ struct spt_scene {
     // launches in flight on several streams do not share one.
     // An entry a stream capture used is baked into that graph, which may be
     // replayed at any time: it is never handed out again (work_captured).
+    // spt_scene_release_captures hands those entries out again once the
+    // caller has destroyed the graphs.  work_mu guards the ring's host state
+    // (launches of one scene from several host threads).
     static constexpr int NWORK = 64;
     int *d_work = nullptr;
+    mutable std::mutex work_mu;
     mutable int work_next = 0;
     mutable unsigned long long work_captured = 0;
     int wide_wpb = 16;                // waves per block of the 8-wide launches (fixed at build: the LDS fit)
@@ -2170,6 +2196,7 @@ int *work_entry(const spt_scene &sc, hipStream_t s)
 {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     const bool capturing = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+    std::lock_guard<std::mutex> lk(sc.work_mu);
     for (int tries = 0; tries < spt_scene::NWORK; tries++) {
         const int k = sc.work_next++ % spt_scene::NWORK;
         if ((sc.work_captured >> k) & 1ull) continue;
@@ -2455,6 +2482,14 @@ extern "C" int spt_scene_destroy(spt_scene *sc)
     return RT_OK;
 }
 
+extern "C" int spt_scene_release_captures(const spt_scene *sc)
+{
+    if (!sc) return rtrt::fail(RT_ERR_INVALID, "spt_scene_release_captures: null scene");
+    std::lock_guard<std::mutex> lk(sc->work_mu);
+    sc->work_captured = 0;
+    return RT_OK;
+}
+
 namespace {
 // Adaptive order (SptSched) for one launch: sets g.order / g.cost; returns
 // true if the caller must queue the cost read-back after the launch.
@@ -2648,9 +2683,26 @@ extern "C" int spt_scene_render_list_async(const spt_scene *sc, const rt_camera 
         return rtrt::fail(RT_ERR_INVALID, "spt_scene_render_list_async: need 0 <= ngroups <= spt_group_count(w, h)");
     int rc = check_render_args(camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, 0, h, first_sample,
                                nsamples, mode);
-    if (rc) return rc;
-    return scene_render(sc, camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, 0, h, 1, first_sample,
-                        nsamples, mode, d_counters, stream, d_groups, ngroups, d_group_cost);
+    if (rc || ngroups == 0) return rc;
+    // The list as a set (list_dedup_kernel): repeated entries render once.
+    // Stream-ordered scratch (graph-capturable): ngroups entries + the claim bits.
+    hipStream_t s = (hipStream_t)stream;
+    const size_t bits = sizeof(unsigned) * (size_t)((total + 31) / 32);
+    char *scratch = nullptr;
+    hipError_t e = hipMallocAsync((void **)&scratch, sizeof(int) * (size_t)ngroups + bits, s);
+    if (e == hipSuccess) e = hipMemsetAsync(scratch + sizeof(int) * (size_t)ngroups, 0, bits, s);
+    if (e != hipSuccess) return rtrt::fail_hip(e, "spt_scene_render_list_async scratch");
+    int *d_set = (int *)scratch;
+    const unsigned blocks = (unsigned)std::min((ngroups + 255) / 256, 1024);
+    hipLaunchKernelGGL(rt::smallpt::list_dedup_kernel, dim3(blocks), dim3(256), 0, s, d_groups, ngroups, total,
+                       (unsigned *)(scratch + sizeof(int) * (size_t)ngroups), d_set);
+    rc = rtrt::check_launch("spt list_dedup_kernel");
+    if (rc == RT_OK)
+        rc = scene_render(sc, camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, 0, h, 1, first_sample,
+                          nsamples, mode, d_counters, stream, d_set, ngroups, d_group_cost);
+    e = hipFreeAsync(scratch, s);
+    if (rc == RT_OK && e != hipSuccess) rc = rtrt::fail_hip(e, "spt_scene_render_list_async scratch free");
+    return rc;
 }
 
 namespace {

@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 #include "rt_runtime.h"
+#include "spt_band.h"
 #include <rccl/rccl.h>
 
 namespace {
@@ -181,9 +182,9 @@ extern "C" int spt_multi_create(const rt_sphere *spheres, unsigned nspheres, int
     m->w = w;
     m->h = h;
     m->bands.resize(ngpus);
-    m->brows = (h + ngpus - 1) / ngpus;
+    m->brows = sptband::rows_per_band(h, ngpus);
     const size_t npx = (size_t)w * h;
-    const size_t npad = (size_t)w * m->brows * ngpus;    // colour rows incl. the all-gather's padding
+    const size_t npad = sptband::padded_floats(w, h, ngpus) / 3;   // pixels incl. the all-gather's padding
     int rc = RT_OK;
     for (int k = 0; k < ngpus && rc == RT_OK; k++) {
         Band &b = m->bands[k];
@@ -192,8 +193,7 @@ extern "C" int spt_multi_create(const rt_sphere *spheres, unsigned nspheres, int
         for (int j = 0; j < k; j++)
             if (m->bands[j].device == dev) m->distinct = false;
         b.device = dev;
-        b.s0 = std::min(h, k * m->brows);
-        b.s1 = std::min(h, (k + 1) * m->brows);
+        sptband::span(h, ngpus, k, &b.s0, &b.s1);
         if ((rc = scope.select(dev))) break;
         if ((rc = spt_scene_create(spheres, nspheres, &b.scene))) break;   // checks gfx950 too
         if ((rc = scope.select(dev))) break;
@@ -308,13 +308,14 @@ extern "C" int spt_multi_gather_async(spt_multi *m)
         }
         // One in-place all-gather: rank k sends its band (slot rows
         // [k B, (k+1) B), padded) from where the full buffer holds it.
-        const size_t cnt = 3 * px_off(*m, m->brows);
+        const size_t cnt = sptband::gather_count(m->w, m->h, n);
         ncclResult_t ne = r->group_start();
         if (ne != ncclSuccess) return fail_nccl(r, ne, "ncclGroupStart");
         for (int k = 0; k < n && ne == ncclSuccess; k++) {
             Band &b = m->bands[k];
             if ((rc = scope.select(b.device))) { (void)r->group_end(); return rc; }
-            ne = r->all_gather(b.d_col + (size_t)k * cnt, b.d_col, cnt, ncclFloat32, m->comms[k], b.stream);
+            ne = r->all_gather(b.d_col + sptband::send_offset(m->w, m->h, n, k), b.d_col, cnt, ncclFloat32,
+                               m->comms[k], b.stream);
         }
         ncclResult_t ge = r->group_end();
         if (ne != ncclSuccess) return fail_nccl(r, ne, "ncclAllGather");

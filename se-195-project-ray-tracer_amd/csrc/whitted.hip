@@ -1347,7 +1347,10 @@ int render_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xrgb, int 
     // once the first's root grid is dispatched (~0.37 ms in at 1080p), so
     // with equal slabs the second ends ~0.16 ms after the first
     // (profiles/r03/whitted_two_stream_timeline.txt).  The first takes p of
-    // every p + q row groups (RT_WHITTED_SPLIT=p,q; 1,1: equal).
+    // every p + q row groups (RT_WHITTED_SPLIT=p,q; 1,1: equal).  The
+    // two-arena memory bound above holds for the equal split only: an
+    // unequal one gives the larger slab p / (p + q) of the groups, up to
+    // 2 max(p, q) / (p + q) of a half arena (an A/B hook; the default is 1,1).
     int sp_p = 1, sp_q = 1;
     if (nstream == 2 && nslab == 2) {
         sp_p = WF_SPLIT_P;

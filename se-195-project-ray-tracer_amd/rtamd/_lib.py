@@ -19,7 +19,7 @@ SPT_COUNT_RAYS = 0x100
 EXPORTS = ("rt_last_error", "rt_device_count", "rt_set_device", "rt_release", "rt_cached_bytes",
            "rt_host_alloc", "rt_host_free",
            "rtw_render", "rtw_render_async", "rtw_render_ocl", "rtw_render_ocl_async", "spt_render", "spt_render_async", "spt_seed_fill",
-           "spt_scene_create", "spt_scene_destroy", "spt_scene_render_async", "spt_scene_render_groups_async",
+           "spt_scene_create", "spt_scene_destroy", "spt_scene_release_captures", "spt_scene_render_async", "spt_scene_render_groups_async",
            "spt_group_count", "spt_scene_render_list_async", "spt_groups_pack_async", "spt_groups_unpack_async",
            "spt_pack_pixels_async",
            "spt_multi_create", "spt_multi_destroy", "spt_multi_set_scene", "spt_multi_bands", "spt_multi_upload",
@@ -101,6 +101,8 @@ def lib():
     L.spt_seed_fill.argtypes = [vp, C.c_size_t, u]
     L.spt_scene_create.argtypes = [vp, u, C.POINTER(vp)]
     L.spt_scene_destroy.argtypes = [vp]
+    if hasattr(L, "spt_scene_release_captures"):
+        L.spt_scene_release_captures.argtypes = [vp]
     L.spt_scene_render_async.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, i, u64p, vp]
     if hasattr(L, "spt_scene_render_groups_async"):
         L.spt_scene_render_groups_async.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, i, u64p, vp]

@@ -195,6 +195,14 @@ class ListGather:
         self.rank, self.world, self.w, self.h = rank, world, w, h
         self.colors, self.pixels, self.pack = colors, pixels, pack
         self.pack_groups, self.unpack_groups = pack_groups, unpack_groups
+        if len(lists) != world:
+            raise ValueError("ListGather: %d lists for %d ranks" % (len(lists), world))
+        flat = [int(g) for x in lists for g in x]
+        ng = group_count(w, h)
+        if len(set(flat)) != len(flat) or any(not 0 <= g < ng for g in flat):
+            # a group owned twice would be unpacked from two shares in rank
+            # order: the frame would depend on which rank unpacks last
+            raise ValueError("ListGather: the lists must be disjoint sets of groups in [0, %d)" % ng)
         dev = colors.device
         self.maxn = max(len(x) for x in lists)
         self.counts = [len(x) for x in lists]

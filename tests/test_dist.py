@@ -135,4 +135,18 @@ def test_balanced_partition_properties():
         loads = [int(costs[p].sum()) for p in parts]
         assert max(loads) - min(loads) <= costs.max()
     assert rd.interleaved_groups(1, 4, 1920, 1080)[:3] == [60, 61, 62]
+
+
+def test_list_gather_refuses_overlapping_lists():
+    """ListGather's lists must partition groups: a group in two ranks' lists
+    (or twice in one), or outside the frame, is refused up front."""
+    import torch
+    from rtamd import dist as rd
+    w, h = 48, 32
+    col, px = torch.zeros(3 * w * h), torch.zeros(w * h, dtype=torch.int32)
+    ng = rd.group_count(w, h)
+    rd.ListGather(col, px, 0, 2, w, h, [list(range(0, ng, 2)), list(range(1, ng, 2))], pack=lambda: None)
+    for bad in ([[0, 1], [1, 2]], [[0, 0], [1]], [[0], [ng]], [[0], [-1]], [[0]]):
+        with pytest.raises(ValueError):
+            rd.ListGather(col, px, 0, 2, w, h, bad, pack=lambda: None)
     assert sum(len(rd.interleaved_groups(k, 3, 197, 61)) for k in range(3)) == rd.group_count(197, 61)

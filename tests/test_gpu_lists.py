@@ -116,6 +116,63 @@ def test_list_costs_and_bad_arguments(rt):
                                          None, None, st) == rt._lib.RT_ERR_INVALID
 
 
+@pytest.mark.parametrize("kind", ["cornell", "complex"])
+def test_list_repeated_entries_render_once(rt, kind):
+    """A list naming groups more than once (and out-of-range entries) is
+    taken as a set: the frame equals the same groups listed once (a group
+    rendered twice with first_sample > 0 would fold its samples into the
+    accumulator twice), so do the counters, and each group's wave time is
+    added to its cost entry once (a repeat would roughly double it).  The
+    whole frame as a list equals the full-frame render."""
+    import torch
+    w, h = 160, 96
+    S, n, cam = _scene(rt, kind, w, h)
+    sc = rt.SmallptScene(S, n)
+    dev = torch.device("cuda", 0)
+    seeds0 = torch.from_numpy(rt.scenes.seeds(w, h).view(np.int32)).to(dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    L = rt.lib()
+    ng = L.spt_group_count(w, h)
+
+    def frame(lst, cost=None):
+        f = _Frame(torch, dev, w, h, seeds0)
+        if lst is None:
+            rt.check(L.spt_scene_render_async(sc.handle, C.byref(cam), f.col.data_ptr(), seeds0.data_ptr(),
+                                              f.seeds.data_ptr(), f.px.data_ptr(), w, h, 0, h, 0, 2, 0,
+                                              f.cnt.data_ptr(), st))
+            rt.check(L.spt_scene_render_async(sc.handle, C.byref(cam), f.col.data_ptr(), f.seeds.data_ptr(),
+                                              f.seeds.data_ptr(), f.px.data_ptr(), w, h, 0, h, 2, 2, 0,
+                                              f.cnt.data_ptr(), st))
+        else:
+            d = torch.tensor(lst, dtype=torch.int32, device=dev)
+            rt.check(L.spt_scene_render_list_async(sc.handle, C.byref(cam), f.col.data_ptr(), seeds0.data_ptr(),
+                                                   f.seeds.data_ptr(), f.px.data_ptr(), w, h, d.data_ptr(),
+                                                   len(lst), 0, 2, 0, f.cnt.data_ptr(), None, st))
+            rt.check(L.spt_scene_render_list_async(sc.handle, C.byref(cam), f.col.data_ptr(), f.seeds.data_ptr(),
+                                                   f.seeds.data_ptr(), f.px.data_ptr(), w, h, d.data_ptr(),
+                                                   len(lst), 2, 2, 0, f.cnt.data_ptr(),
+                                                   cost.data_ptr() if cost is not None else None, st))
+        torch.cuda.synchronize()
+        return f
+
+    ref = frame(None)
+    rng = np.random.default_rng(5)
+    base = [int(g) for g in rng.permutation(ng)]
+    assert frame(base).same(ref, torch)
+    cover = base[: ng // 2]                        # half the frame, then repeats (a list is <= ng long)
+    lst = cover + [int(g) for g in rng.choice(cover, ng // 4)] + [-1, ng]
+    rng.shuffle(lst)
+    c1 = torch.zeros(ng, dtype=torch.int32, device=dev)
+    c2 = torch.zeros(ng, dtype=torch.int32, device=dev)
+    once = frame(cover, c1)
+    got = frame(lst, c2)
+    assert got.same(once, torch) and got.cnt.tolist() == once.cnt.tolist()
+    if kind == "complex":                     # costs are recorded by the hierarchy kernels
+        a, b = c1.cpu().numpy().astype(np.float64)[cover], c2.cpu().numpy().astype(np.float64)[cover]
+        assert (a > 0).all() and (b > 0).all()
+        assert np.median(b / a) < 1.5, np.median(b / a)
+
+
 @pytest.mark.parametrize("w,h", [(1920, 1080), (197, 61), (33, 9)])
 def test_groups_pack_unpack(rt, w, h):
     """spt_groups_pack_async == the host-side slot map (rtamd.dist.group_slots)

@@ -355,6 +355,55 @@ def test_graph_replay_survives_order_changes(rt):
         assert (a.cpu().numpy().view(np.uint32) == b.cpu().numpy().view(np.uint32)).all()
 
 
+def test_capture_limit_and_release(rt):
+    """A hierarchy scene holds 64 work-counter entries and a captured launch
+    keeps its entry for the graph's life: with 64 captured launches alive the
+    next launch is refused (RT_ERR_INVALID, nothing launched); once the graph
+    is destroyed spt_scene_release_captures hands the entries out again, and
+    a new capture replays to the uncaptured frame's bits."""
+    import ctypes as C
+    import torch
+    w, h = 64, 16
+    spheres, n, cam = rt.scenes.complex10k()
+    rt.scenes.update_camera(cam, w, h)
+    sc = rt.SmallptScene(spheres, n)
+    dev = torch.device("cuda", 0)
+    seeds0 = torch.from_numpy(rt.scenes.seeds(w, h).view(np.int32)).to(dev)
+    L = rt.lib()
+    b = (torch.zeros(3 * w * h, dtype=torch.float32, device=dev), torch.zeros_like(seeds0),
+         torch.zeros(w * h, dtype=torch.int32, device=dev))
+
+    def launch(buf):
+        return L.spt_scene_render_async(sc.handle, C.byref(cam), buf[0].data_ptr(), seeds0.data_ptr(),
+                                        buf[1].data_ptr(), buf[2].data_ptr(), w, h, 0, h, 0, 1, 0, None,
+                                        torch.cuda.current_stream(dev).cuda_stream)
+
+    for _ in range(3):
+        rt.check(launch(b))
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="relaxed"):
+        rcs = [launch(b) for _ in range(64)]
+    assert rcs == [0] * 64
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2, capture_error_mode="relaxed"):
+        assert launch(b) == rt._lib.RT_ERR_INVALID
+    assert launch(b) == rt._lib.RT_ERR_INVALID        # (uncaptured launches need an entry too)
+    del g, g2
+    torch.cuda.synchronize()
+    rt.check(L.spt_scene_release_captures(sc.handle))
+    gb = tuple(torch.zeros_like(t) for t in b)
+    g3 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g3, capture_error_mode="relaxed"):
+        rt.check(launch(gb))
+    g3.replay()
+    ref = tuple(torch.zeros_like(t) for t in b)
+    rt.check(launch(ref))
+    torch.cuda.synchronize()
+    for a, r in zip(gb, ref):
+        assert torch.equal(a.view(torch.int32), r.view(torch.int32))
+
+
 def _bvh_vs_scan(rt, monkeypatch, spheres, n, cam, w, h, spp, mode=0):
     """Renders with the 8-wide hierarchy, the binary hierarchy (RT_SPT_WIDE=0)
     and the full scan (RT_SPT_NO_BVH), each with and without the work
