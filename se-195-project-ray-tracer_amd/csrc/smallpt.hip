@@ -340,7 +340,19 @@ struct BvhWalk {
 #ifdef RT_SPT_TRACE
     unsigned tr_leaf, tr_trips, tr_leafruns;   // tools-only phase stamps (s_memtime cycles, counts)
 #endif
+#ifdef RT_SPT_PROF
+    unsigned pf_l[3], pf_w[3];   // tools-only: lanes / wave-executions of wide_walk calls, node steps, leaf passes
+#endif
 };
+#ifdef RT_SPT_PROF
+#define WALK_PROF(W, b)                                                                    \
+    do {                                                                                   \
+        (W).pf_l[b]++;                                                                     \
+        if ((int)(threadIdx.x & 63) == __builtin_ctzll(__builtin_amdgcn_read_exec())) (W).pf_w[b]++; \
+    } while (0)
+#else
+#define WALK_PROF(W, b) do {} while (0)
+#endif
 
 // Starts a query: the "always" spheres, then the walk from the root.
 // Nearest hit (shadow = false): t = 1e20f on entry; any hit: t = maxt.
@@ -712,8 +724,10 @@ __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigne
     unsigned *my = stk + (threadIdx.x & 63);
     const int n0 = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true));   // lanes in this call
     int trips = 0;
+    WALK_PROF(W, 0);
     while (true) {
         if (m != 0 && pend2 == 0) {
+            WALK_PROF(W, 1);
             int cw;
             if (cur < 0) {
                 cw = 0;                                  // the root
@@ -762,6 +776,7 @@ __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigne
         W.tr_leafruns++;
 #endif
         if (pend != 0) {
+            WALK_PROF(W, 2);
             const int f = pend & 0xffffff, c = pend >> 24, c4 = c < BVH_LEAF_MAX ? c : BVH_LEAF_MAX;
             float4 g[BVH_LEAF_MAX];
 #pragma unroll
@@ -1195,7 +1210,8 @@ struct Counts { unsigned isect, isectp, samples; unsigned long long tests; };
 // (iterations in which at least one lane of the wave did).  Never in the
 // product build.
 #ifdef RT_SPT_PROF
-enum { PB_ITER, PB_SHADOW, PB_NEAREST, PB_DIFF, PB_SPEC, PB_REFR, PB_LIGHT, PB_BOUNCE, PB_DONE, PB_N };
+enum { PB_ITER, PB_SHADOW, PB_NEAREST, PB_DIFF, PB_SPEC, PB_REFR, PB_LIGHT, PB_BOUNCE, PB_DONE,
+       PB_WCALL, PB_WSTEP, PB_WLEAF, PB_WSHADE, PB_N };
 __device__ unsigned long long g_spt_prof[2 * PB_N];
 #define SPT_PROF(b)                                                                        \
     do {                                                                                   \
@@ -1253,6 +1269,13 @@ constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2, GEO_WIDE = 3;
 #endif
 #ifndef RT_SPT_COOP_G
 #define RT_SPT_COOP_G 8     // lanes per pixel of the cooperative walk (heavy tiles of the 8-wide kernels): 8 or 4
+#endif
+#ifndef RT_SPT_REFILL
+#define RT_SPT_REFILL 0     // 8-wide persistent kernels: a lane whose pixel is done takes the next pixel (A/B: 1;
+                            // 2: not in waves that started on a routed heavy tile)
+#endif
+#ifndef RT_SPT_REFILL_BATCH
+#define RT_SPT_REFILL_BATCH 1   // refill once this many lanes are free (or no lane of the wave has a pixel)
 #endif
 #ifndef RT_SPT_GSTORE
 #define RT_SPT_GSTORE 1     // hierarchy kernels: a group's outputs stored whole by its last wave (A/B: 0)
@@ -1368,9 +1391,11 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // (work[1]): a heavy tile's SIMD shares its issue slots with lighter,
     // lower-priority waves instead of with three other heavy tiles; every
     // wave then takes the rest in order (work[0]).
+    // (by the wave's first active lane: refill claims fetch from inside the
+    // pixel loop, where lanes that ran out of work have left)
     const auto fetch = [&]() {
         int v = 0;
-        if (lane == 0) {
+        if (lane == __builtin_ctzll(__builtin_amdgcn_read_exec())) {
             v = -1;
             if (wave < hw && n1 > 0) {
                 const int hv = atomicAdd(work + 2, 1);
@@ -1382,7 +1407,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             }
             if (v < 0) v = (n1 << hs) + n2 + atomicAdd(work, 1);
         }
-        return __shfl(v, 0, 64);
+        return __builtin_amdgcn_readfirstlane(v);
     };
     int f = ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) * 4 + (wave & 3);
     if (PERSIST) f = __builtin_amdgcn_readfirstlane(fetch());
@@ -1419,30 +1444,52 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         if ((threadIdx.x & 255) == 0) *(int *)(GS_BASE() + 6144) = 0;
         __syncthreads();
     }
-    const int x = (tile % tiles_x) * 8 + (li & 7);
+    int x = (tile % tiles_x) * 8 + (li & 7);
     // gstride > 1: the window is every gstride-th 8-row group from row_begin
     // (spt_scene_render_groups_async, multi-GPU load balance).
-    const int y = row_begin + (tile / tiles_x) * 8 * gstride + (li >> 3);
+    int y = row_begin + (tile / tiles_x) * 8 * gstride + (li >> 3);
+    // Refill (8-wide persistent kernels, items past the cooperative / split
+    // tier): the wave starts on this item's 64 pixels, and from then on a
+    // lane whose pixel has taken all its samples stores it and takes the next
+    // pixel of the dispatch sequence (the rest of the wave's current item,
+    // then further items), until the window's work is gone.  A tile of
+    // configs[4] mixes pixels whose sample chains differ several-fold (sky
+    // beside the fractal): waiting for the tile's slowest pixel left 28 % of
+    // the lanes idle (tools/c4_lanes.py).  Every pixel's computation is
+    // unchanged -- only which lane runs it, and when.
+    const bool refill = RT_SPT_REFILL && PERSIST && !heavy_ && (RT_SPT_REFILL == 1 || f >= (n1 << hs) + n2);
 #ifdef RT_SPT_TRACE
-    const bool active = gvalid && lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end &&
-                        (g_spt_only_group < 0 || grp == g_spt_only_group);
+    bool active = gvalid && lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end &&
+                  (g_spt_only_group < 0 || grp == g_spt_only_group);
     unsigned tr_walk = 0, tr_leaf = 0, tr_trips = 0, tr_leafruns = 0, tr_queries = 0;
     const unsigned long long tr_c0 = __builtin_amdgcn_s_memtime();
     const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();
 #else
-    const bool active = gvalid && lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end;
+    bool active = gvalid && lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end;
 #endif
 
 #ifdef RT_SPT_TRACE
     unsigned tr_iters = 0;
 #endif
-    if (active) {
-        const int i = (h - y - 1) * w + x;                      // smallptCPU.cpp:86
-        uint32_t s0 = seeds_in[2 * (size_t)i], s1 = seeds_in[2 * (size_t)i + 1];
+    if (active || refill) {
+        int i = (h - y - 1) * w + x;                            // smallptCPU.cpp:86
+        uint32_t s0 = 0, s1 = 0;
         v3 col = mk(0.f, 0.f, 0.f);
-        if (first_sample > 0)
-            col = mk(colors[3 * (size_t)i], colors[3 * (size_t)i + 1], colors[3 * (size_t)i + 2]);
+        if (active) {
+            s0 = seeds_in[2 * (size_t)i];
+            s1 = seeds_in[2 * (size_t)i + 1];
+            if (first_sample > 0)
+                col = mk(colors[3 * (size_t)i], colors[3 * (size_t)i + 1], colors[3 * (size_t)i + 2]);
+        }
         const float invW = 1.f / w, invH = 1.f / h;             // :80-81
+        // Refill state: the lane's pixel is px_ok (its group pgrp, started at
+        // pix_t0), exhausted once the window has no pixel left for it; the
+        // wave's dispatch cursor is item rf_f, pixel rf_p (wave-uniform: only
+        // updated at the loop top, where every lane still looping is active).
+        bool px_ok = active, exhausted = false;
+        int pgrp = grp;
+        unsigned pix_t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
+        int rf_f = f, rf_p = 64 >> sp_;
 
         // Per-lane path state.  Every loop iteration issues exactly ONE ray
         // query for every live lane -- the path ray (nearest hit) or, while a
@@ -1476,11 +1523,14 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         float lmax = 0.f;      // shadow ray maxt (len - EPSILON)
         float lw = 0.f;        // that light's weight s (geomfunc.h:159)
         int li = 0;
-        int k = 0;
-        bool need_cam = nsamples > 0, need_bounce = false;
+        int k = active ? 0 : nsamples;      // (refill: a lane without a pixel takes one first)
+        bool need_cam = active && nsamples > 0, need_bounce = false;
         BvhWalk walk;          // GEO_BVH: the current query's walk state
 #ifdef RT_SPT_TRACE
         walk.tr_leaf = walk.tr_trips = walk.tr_leafruns = 0;
+#endif
+#ifdef RT_SPT_PROF
+        for (int b = 0; b < 3; b++) walk.pf_l[b] = walk.pf_w[b] = 0;
 #endif
         bool walking = false;  //   and whether it is suspended mid-walk
         constexpr float nc = 1.f, nt = 1.5f;
@@ -1498,6 +1548,66 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         else __builtin_amdgcn_s_setprio(2);
 #endif
         while (true) {
+            if (refill) {
+                // ---- refill: lanes whose pixel is done store it, then take
+                // the next pixels of the wave's dispatch sequence
+                const bool want = k >= nsamples && !exhausted;
+                const unsigned long long wm = __builtin_amdgcn_ballot_w64(want);
+                if (wm && (__builtin_popcountll(wm) >= RT_SPT_REFILL_BATCH || wm == __builtin_amdgcn_read_exec())) {
+                    if (want && px_ok) {
+                        if (nsamples > 0) {
+                            colors[3 * (size_t)i] = col.x;
+                            colors[3 * (size_t)i + 1] = col.y;
+                            colors[3 * (size_t)i + 2] = col.z;
+                            pixels[(size_t)y * w + x] =
+                                (uint32_t)(to_int(col.x) | (to_int(col.y) << 8) | (to_int(col.z) << 16));
+                        }
+                        seeds_out[2 * (size_t)i] = s0;
+                        seeds_out[2 * (size_t)i + 1] = s1;
+                        if (SCHED && group_cost)        // the pixel's duration, summed per group
+                            atomicAdd(&group_cost[pgrp], (unsigned)__builtin_amdgcn_s_memrealtime() - pix_t0);
+                    }
+                    const unsigned long long need = __builtin_amdgcn_ballot_w64(want);
+                    const int ncl = __builtin_popcountll(need);
+                    const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+                    const bool more = rf_p + ncl > 64;
+                    const int f2 = more ? fetch() : nwork;
+                    if (want) {
+                        const int pos = rf_p + rank;
+                        const int mf = pos < 64 ? rf_f : f2, mp = pos < 64 ? pos : pos - 64;
+                        px_ok = false;
+                        if (mf >= nwork) {
+                            exhausted = true;
+                        } else {
+                            const int it = mf - (n1 << hs) + n1, sl = it >> 2;
+                            const int g = group_order ? (sl < nslots ? group_order[sl] : -1) : sl;
+                            const int tl = g * 4 + (it & 3);
+                            x = (tl % tiles_x) * 8 + (mp & 7);
+                            y = row_begin + (tl / tiles_x) * 8 * gstride + (mp >> 3);
+                            if ((unsigned)g < (unsigned)((ntiles + 3) >> 2) && tl < ntiles && x < w && y < row_end) {
+                                i = (h - y - 1) * w + x;
+                                s0 = seeds_in[2 * (size_t)i];
+                                s1 = seeds_in[2 * (size_t)i + 1];
+                                col = mk(0.f, 0.f, 0.f);
+                                if (first_sample > 0)
+                                    col = mk(colors[3 * (size_t)i], colors[3 * (size_t)i + 1], colors[3 * (size_t)i + 2]);
+                                k = 0;
+                                need_cam = nsamples > 0;
+                                px_ok = true;
+                                pgrp = g;
+                                pix_t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
+                            }
+                        }
+                    }
+                    if (more) {
+                        rf_f = f2;
+                        rf_p += ncl - 64;
+                    } else {
+                        rf_p += ncl;
+                    }
+                }
+            }
             // ---- pass B: DIFF bounce (geomfunc.h:229-269) or camera ray
             // (smallptCPU.cpp:89-105).  Both draw two randoms and normalise
             // one vector.
@@ -1538,7 +1648,10 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 }
                 need_bounce = need_cam = false;
             }
-            if (k >= nsamples) break;
+            if (k >= nsamples) {
+                if (!refill || exhausted) break;
+                continue;                       // (a pixel past the frame's edge: claim again)
+            }
 #if RT_SPT_PRIO
             // Progress-levelled issue priority.  The SIMD arbitrates VALU issue
             // by priority, then age, so waves that start together finish one
@@ -1547,7 +1660,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             // of its samples drops one priority level, letting the waves
             // behind it catch up: co-resident waves stay level and finish
             // together.  (s_setprio only reorders issue; results unchanged.)
-            if (!wave_any(k < prio_next)) {
+            if (!refill && !wave_any(k < prio_next)) {
                 prio_level++;
                 prio_next = prio_level < 3 ? (nsamples * ((prio_sched >> (8 * prio_level)) & 255)) >> 8 : nsamples;
                 if (prio_level == 1 && top3) __builtin_amdgcn_s_setprio(2);
@@ -1619,6 +1732,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 tr_walk += (unsigned)(__builtin_amdgcn_s_memtime() - tr_w0);
 #endif
                 if (walking) continue;
+                SPT_PROF(PB_WSHADE);
                 t = walk.t;
                 id = walk.id;
                 first = id;                 // any hit: the highest occluder (COUNT)
@@ -1866,7 +1980,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             }
             gs_seed[r * 64 + 2 * c] = s0;
             gs_seed[r * 64 + 2 * c + 1] = s1;
-        } else if (lead) {
+        } else if (lead && !refill) {            // (refill: stored as each pixel finished)
             if (nsamples > 0) {
                 colors[3 * (size_t)i] = col.x;
                 colors[3 * (size_t)i + 1] = col.y;
@@ -1877,6 +1991,12 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             seeds_out[2 * (size_t)i] = s0;
             seeds_out[2 * (size_t)i + 1] = s1;
         }
+#ifdef RT_SPT_PROF
+        for (int b = 0; b < 3; b++) {
+            prof_l[PB_WCALL + b] += walk.pf_l[b];
+            prof_w[PB_WCALL + b] += walk.pf_w[b];
+        }
+#endif
 #ifdef RT_SPT_TRACE
         if (GEO == GEO_BVH || GEO == GEO_WIDE) {
             tr_leaf = walk.tr_leaf;
@@ -1929,7 +2049,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         }
     }
 #undef GS_BASE
-    if (SCHED && group_cost && gvalid && lane == 0)   // this tile's duration (100 MHz ticks), summed per group
+    if (SCHED && group_cost && gvalid && lane == 0 && !refill)   // this tile's duration (100 MHz ticks), summed per group
         atomicAdd(&group_cost[grp], (unsigned)(__builtin_amdgcn_s_memrealtime() - t_start));
 #ifdef RT_SPT_TRACE
     {
@@ -1960,7 +2080,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         flush_counters<4>(counters, c);
         cnt = Counts{0, 0, 0, 0};
     }
-    if (!PERSIST) break;
+    if (!PERSIST || refill) break;          // (refill: the wave took pixels until the window ran out)
     f = __builtin_amdgcn_readfirstlane(fetch());
     }   // work items
     if (CALLS) {
@@ -2555,9 +2675,14 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
     }
     if (q.state == 2) {
         g.order = q.d_order;
-        int heavy = sc.cus / 4;                         // a heavy group (a wave per SIMD) on every 4th CU
-                                                        // (measured: 0, cus/4, cus/2, cus, 4cus groups: 32.6,
-                                                        // 31.8, 32.2, 33.2, 32.6 ms, configs[4])
+        // Heaviest groups kept at the top issue priority throughout: none
+        // since round 5 (configs[4], same box: cus/4 groups 24.7-26.3 ms, 16
+        // 24.5-25.6, 0 24.2 ms; N = 8 windows 0/8 11.2 -> 10.2, 3/8 12.2 ->
+        // 11.0 ms; N = 4, 2 level -- profiles/r05/c4_heavy_prio_sweep.log):
+        // every wave levels its priority down by progress, and a wave held
+        // at the top starves its SIMD's others.  (Round 2, binary walk:
+        // cus/4 was best.)  RT_SPT_HEAVY=n: A/B.
+        int heavy = 0;
         if (const char *he = getenv("RT_SPT_HEAVY")) heavy = atoi(he);
         g.heavy16 = std::min(std::max((heavy + 15) / 16, 0), 255);
         return false;
@@ -2604,7 +2729,9 @@ int scene_render(const spt_scene *sc, const rt_camera *camera, float *d_colors, 
         grid.order = d_list;
         grid.cost = sc->bvh.node ? d_cost : nullptr;
         grid.tiers = d_cost == nullptr;
-        grid.heavy16 = d_cost ? 0 : std::min(std::max((sc->cus / 4 + 15) / 16, 0), 255);
+        grid.heavy16 = 0;                 // (no group held at the top priority: see sched_before)
+        if (const char *he = getenv("RT_SPT_HEAVY"))
+            if (!d_cost) grid.heavy16 = std::min(std::max((atoi(he) + 15) / 16, 0), 255);
     } else {
         record = sched_before(*sc, grid, s, w, h, row_begin, row_end, gstride, nsamples, base, *camera,
                               d_counters && !(mode & SPT_COUNT_RAYS));

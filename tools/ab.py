@@ -41,19 +41,30 @@ def child():
             from rtamd import dist as rdist
             k, N = (int(v) for v in os.environ["BAND"].split("/"))
             r0, r1 = rdist.row_band(k, N, H)
-        S, n = rtamd.scenes.cornell()
-        cam = rtamd.scenes.cornell_camera(W, H)
+        if os.environ.get("SCENE") == "c4":        # BASELINE configs[4] (8-wide hierarchy kernel)
+            S, n, cam = rtamd.scenes.complex10k()
+            rtamd.scenes.update_camera(cam, W, H)
+        else:
+            S, n = rtamd.scenes.cornell()
+            cam = rtamd.scenes.cornell_camera(W, H)
         sc = rtamd.SmallptScene(S, n)
         seeds0 = torch.from_numpy(rtamd.scenes.seeds(W, H).view(np.int32)).to(dev)
         seeds = torch.empty_like(seeds0)
         col = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
         px = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        grp = os.environ.get("GROUP")              # k/N: the interleaved share of rank k of N
 
         def run():
+            if grp:
+                k, N = (int(v) for v in grp.split("/"))
+                rtamd.check(L.spt_scene_render_groups_async(sc.handle, C.byref(cam), col.data_ptr(),
+                                                            seeds0.data_ptr(), seeds.data_ptr(), px.data_ptr(),
+                                                            W, H, k, N, 0, SPP, 0, None, st.cuda_stream))
+                return
             rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
                                                  seeds.data_ptr(), px.data_ptr(), W, H, r0, r1, 0, SPP, 0,
                                                  None, st.cuda_stream))
-    for _ in range(int(os.environ.get("WARM", "1"))):
+    for _ in range(int(os.environ.get("WARM", "3" if os.environ.get("SCENE") == "c4" else "1"))):
         run()
     torch.cuda.synchronize()
     ts = []
@@ -65,13 +76,14 @@ def child():
         torch.cuda.synchronize()
         ts.append(a.elapsed_time(b))
     if os.environ.get("PROF"):      # block counters of a tools-only instrumented build
-        buf = (C.c_ulonglong * 18)()
+        names = ["iter", "shadow", "nearest", "diff", "spec", "refr", "light", "bounce", "done",
+                 "wcall", "wstep", "wleaf", "wshade"]
+        buf = (C.c_ulonglong * (2 * len(names)))()
         L.spt_prof_read(buf)
-        names = ["iter", "shadow", "nearest", "diff", "spec", "refr", "light", "bounce", "done"]
         for b, nm in enumerate(names):
             lanes, waves = buf[2 * b], buf[2 * b + 1]
             print("  %-8s lanes %14d waves %12d lanes/wave-exec %.1f" % (nm, lanes, waves, lanes / max(waves, 1)))
-    print("%s %s %s min %.3f med %.3f ms" % (os.environ.get("KERNEL", "smallpt"), os.environ.get("BAND", ""),
+    print("%s %s %s min %.3f med %.3f ms" % (os.environ.get("KERNEL", "smallpt"), os.environ.get("BAND", os.environ.get("GROUP", "")),
                                             os.environ.get("VARIANT", "?"), min(ts), float(np.median(ts))),
           flush=True)
 
