@@ -1144,6 +1144,9 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
                 // before its inner children.
                 bool occl = false;
                 unsigned l = lm;
+#ifdef RT_SPT_TRACE
+                const unsigned long long tr_l0 = l ? __builtin_amdgcn_s_memtime() : 0ull;
+#endif
                 while (l) {
                     int fa[RT_SPT_COOP_NL], ca[RT_SPT_COOP_NL];
 #pragma unroll
@@ -1157,11 +1160,17 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
                             ca[q] = wq >> 24;
                         }
                     }
+#ifdef RT_SPT_TRACE
+                    W.tr_leafruns++;
+#endif
                     if (leaf_coop<COUNT, G, RT_SPT_COOP_NL>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id)) {
                         occl = true;
                         break;
                     }
                 }
+#ifdef RT_SPT_TRACE
+                if (lm) W.tr_leaf += (unsigned)(__builtin_amdgcn_s_memtime() - tr_l0);
+#endif
                 const unsigned nm = hm & ~lm;
                 if (occl) {
                     m = 0;
