@@ -1279,6 +1279,9 @@ constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2, GEO_WIDE = 3;
 #ifndef RT_SPT_COOP_G
 #define RT_SPT_COOP_G 8     // lanes per pixel of the cooperative walk (heavy tiles of the 8-wide kernels): 8 or 4
 #endif
+#ifndef RT_WIDE_SPREAD
+#define RT_WIDE_SPREAD 1    // 8-wide persistent kernels: first tier-1 sub-items assigned wave-major (A/B: 0)
+#endif
 #ifndef RT_SPT_REFILL
 #define RT_SPT_REFILL 0     // 8-wide persistent kernels: a lane whose pixel is done takes the next pixel (A/B: 1;
                             // 2: not in waves that started on a routed heavy tile)
@@ -1402,12 +1405,14 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // wave then takes the rest in order (work[0]).
     // (by the wave's first active lane: refill claims fetch from inside the
     // pixel loop, where lanes that ran out of work have left)
+    // (RT_WIDE_SPREAD below: the first min(hw, waves per block) x #blocks tier-1 sub-items are assigned statically)
+    const int nstatic = (PERSIST && RT_WIDE_SPREAD) ? min(min(hw, (int)(blockDim.x >> 6)) * (int)gridDim.x, n1 << hs) : 0;
     const auto fetch = [&]() {
         int v = 0;
         if (lane == __builtin_ctzll(__builtin_amdgcn_read_exec())) {
             v = -1;
             if (wave < hw && n1 > 0) {
-                const int hv = atomicAdd(work + 2, 1);
+                const int hv = atomicAdd(work + 2, 1) + nstatic;
                 if (hv < (n1 << hs)) v = hv;
             }
             if (v < 0 && wave < 4 && n2 > 0) {
@@ -1419,7 +1424,15 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         return __builtin_amdgcn_readfirstlane(v);
     };
     int f = ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) * 4 + (wave & 3);
-    if (PERSIST) f = __builtin_amdgcn_readfirstlane(fetch());
+    if (PERSIST) {
+        // RT_WIDE_SPREAD: the first tier-1 sub-item of wave w of block b is
+        // w * #blocks + b, not the next one a shared counter hands out: the
+        // heaviest tiles' sub-items (dispatch order) land one per CU, beside
+        // lighter ones on their SIMD, where the counter gave a whole heavy
+        // tile's rows to the waves of the first block to start.
+        const int fs = wave * (int)gridDim.x + (int)blockIdx.x;
+        f = (RT_WIDE_SPREAD && wave < hw && fs < (n1 << hs)) ? fs : __builtin_amdgcn_readfirstlane(fetch());
+    }
     while (!PERSIST || f < nwork) {
     const bool heavy_ = f < (n1 << hs);
     // hs = 3 (COOP, G = 8): a heavy tile's 8 sub-items are 8 rows of 8 pixels

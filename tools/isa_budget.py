@@ -35,7 +35,7 @@ def ranges(path):
         raise SystemExit("marker not found: %s" % pat)
     loop = find(r"^\s+while \(true\) \{\s*$", find(r"^render_kernel\("))
     pb = find(r"// ---- pass B", loop)
-    q0 = find(r"if \(k >= nsamples\) break;", pb)
+    q0 = find(r"if \(k >= nsamples\) \{", pb)
     hit = find(r"float dp = 0.f, inv_sign = 1.f;", q0)
     pa = find(r"// ---- pass A", hit)
     done = find(r"if \(done\) \{", pa)
