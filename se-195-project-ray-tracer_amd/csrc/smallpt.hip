@@ -855,6 +855,289 @@ __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigne
 }
 
 // ---------------------------------------------------------------------------
+// Block pool of pending walks (RT_WIDE_POOL, uncounted 8-wide kernels).
+// wide_walk leaves a lane idle from the trip its query ends until the call
+// returns, and a lane whose query outlives the call holds its walk in its
+// own registers until its wave calls again: configs[4]'s node steps ran with
+// 31.5 of 64 lanes, its leaf passes with 18.9 (profiles/r05).  Here a walk
+// that outlives the call is parked in LDS -- the query's whole state, one
+// slot per owning lane of the block (threadIdx.x), its stack entries staying
+// where they are (the owner wave's stack region) -- and any lane of the
+// block whose own query is parked (or that has none) takes parked walks
+// from the pool, in the call and whenever it goes idle inside one, and
+// writes each finished walk's (t, id) into the owner's result slot.  A walk's
+// result does not depend on which lane steps it, nor in how many calls: the
+// nearest distance is a minimum with ties to the highest index, the any-hit
+// any occluder, and every trip is the one wide_walk would take from the same
+// state.  The owner picks its result up after a call (shading only its own
+// lanes, as before).
+//
+// LDS, after the stacks (pool_bytes): three planes of 16 B per slot (origin
+// + t, direction, (node + 1) << 8 | mask / sp | shadow << 8 / pend / pend2),
+// bpos, the result (t, id; id = POOL_SENT while pending), and 33 words of
+// flags: bit o of word o >> 5 = slot o parked, bit w of word 32 = word w
+// may be non-zero (set after the word's bit; a claimer that empties a word
+// clears its summary bit, then re-reads the word and sets it again if a
+// push came in between).
+constexpr int POOL_SLOTS = 1024;
+constexpr int POOL_SENT = (int)0x80000000;
+__host__ __device__ constexpr size_t pool_bytes() { return (size_t)POOL_SLOTS * (3 * 16 + 4 + 8) + 64 * 4; }
+struct WidePool {
+    uint4 *p0, *p1, *p2;
+    int *pb;
+    uint2 *res;
+    unsigned *bits;
+};
+__device__ __forceinline__ WidePool pool_carve(char *base)
+{
+    WidePool P;
+    P.p0 = (uint4 *)base;
+    P.p1 = P.p0 + POOL_SLOTS;
+    P.p2 = P.p1 + POOL_SLOTS;
+    P.pb = (int *)(P.p2 + POOL_SLOTS);
+    P.res = (uint2 *)(P.pb + POOL_SLOTS);
+    P.bits = (unsigned *)(P.res + POOL_SLOTS);
+    return P;
+}
+// Position of the r-th (from 0) set bit of v (r < popcount(v)).
+__device__ __forceinline__ int nth_set_bit(unsigned v, int r)
+{
+    int pos = 0;
+#pragma unroll
+    for (int sz = 16; sz >= 1; sz >>= 1) {
+        const unsigned lo = v & ((1u << sz) - 1u);
+        const int c = __builtin_popcount(lo);
+        if (r >= c) {
+            r -= c;
+            v >>= sz;
+            pos += sz;
+        } else {
+            v = lo;
+        }
+    }
+    return pos;
+}
+
+#ifndef RT_WIDE_POOL_REFILL
+#define RT_WIDE_POOL_REFILL 16   // pool walk: claim parked walks once >= REFILL/64 of the call's lanes are idle
+#endif
+
+// One pool call.  fresh: the lane starts a query of its own (W, r: as
+// wide_begin left them; its origin and direction already in its slot); the
+// other lanes of the call take parked walks.  Returns nothing: the owner
+// reads its result slot afterwards.  stk0 / sstride: the block's stack
+// region and one wave's share of it.  opts as wide_walk (budget, batch,
+// stop); refill (sflags bits 8..15): the idle share that triggers a claim.
+__device__ void wide_walk_pool(const BvhView &B, const uint4 *__restrict__ L, unsigned *__restrict__ stk0, int sstride,
+                               const WidePool &P, bool fresh, const ray3 &r, bool shadow0, BvhWalk &W, int opts,
+                               int refill)
+{
+    const int budget = (opts >> 8) & 255, batch = (opts >> 16) & 255, stop = (opts >> 24) & 255;
+    const int lane = threadIdx.x & 63;
+    int owner = fresh ? (int)threadIdx.x : -1;
+    v3 ro = r.o, rd = r.d;
+    float t = W.t;
+    int id = W.id, cur = W.node, pend = W.pend, pend2 = W.pend2, sp = W.sp, bpos = W.bpos;
+    unsigned m = W.m;
+    bool shadow = shadow0;
+    float ix, iy, iz, alpha;
+    int oct;
+    unsigned *my = stk0 + (threadIdx.x >> 6) * sstride + lane;
+    const auto derive = [&]() {
+        const float dx = fabsf(rd.x) < 1e-30f ? copysignf(1e-30f, rd.x) : rd.x;
+        const float dy = fabsf(rd.y) < 1e-30f ? copysignf(1e-30f, rd.y) : rd.y;
+        const float dz = fabsf(rd.z) < 1e-30f ? copysignf(1e-30f, rd.z) : rd.z;
+        ix = __builtin_amdgcn_rcpf(dx);
+        iy = __builtin_amdgcn_rcpf(dy);
+        iz = __builtin_amdgcn_rcpf(dz);
+        const float e = fabsf(rd.x * rd.x + rd.y * rd.y + rd.z * rd.z - 1.f);
+        alpha = e < 0x1p-16f ? BVH_K * (1.04e-3f + __builtin_amdgcn_sqrtf(e + 0x1p-22f)) : 1e30f;
+        oct = (dx < 0.f ? 1 : 0) | (dy < 0.f ? 2 : 0) | (dz < 0.f ? 4 : 0);
+    };
+    derive();
+    const unsigned *Lw = (const unsigned *)L;
+    const int n0 = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true));   // lanes in this call
+    int trips = 0;
+    bool dry = false;                  // the last claim found the pool empty
+    int nb0 = 64;                      // lanes holding a walk after the first claim
+    WALK_PROF(W, 0);
+    while (true) {
+        // ---- claim parked walks for idle lanes (one flag word per claim)
+        const unsigned long long im = __builtin_amdgcn_ballot_w64(owner < 0);
+        if (im && (trips == 0 || 64 * __builtin_popcountll(im) >= refill * n0) && (!dry || (trips & 3) == 0)) {
+            const int lead = __builtin_ctzll(__builtin_amdgcn_read_exec());
+            unsigned got = 0;
+            int wd = 0;
+            if (lane == lead) {
+                const unsigned s = __hip_atomic_load(P.bits + 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (s) {
+                    // (the wave's own two words first, then round the block)
+                    const int st = 2 * (int)(threadIdx.x >> 6) & 31;
+                    wd = (__builtin_ctz((s >> st) | (s << ((32 - st) & 31))) + st) & 31;
+                    const unsigned cw = __hip_atomic_load(P.bits + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const int want_n = __builtin_popcountll(im);
+                    const unsigned want = __builtin_popcount(cw) <= want_n ? cw
+                                                                          : cw & ((1u << nth_set_bit(cw, want_n)) - 1u);
+                    unsigned rest = 0;
+                    if (want) {
+                        const unsigned old = __hip_atomic_fetch_and(P.bits + wd, ~want, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+                        got = old & want;
+                        rest = old & ~want;
+                    }
+                    if (rest == 0) {
+                        __hip_atomic_fetch_and(P.bits + 32, ~(1u << wd), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (__hip_atomic_load(P.bits + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                            __hip_atomic_fetch_or(P.bits + 32, 1u << wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+            }
+            got = __builtin_amdgcn_readfirstlane(got);
+            wd = __builtin_amdgcn_readfirstlane(wd);
+            dry = got == 0;
+            if (got) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
+                if (owner < 0 && rank < __builtin_popcount(got)) {
+                    const int o = 32 * wd + nth_set_bit(got, rank);
+                    const uint4 a = P.p0[o], b = P.p1[o], c = P.p2[o];
+                    bpos = P.pb[o];
+                    ro = mk(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z));
+                    t = __uint_as_float(a.w);
+                    rd = mk(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z));
+                    id = (int)b.w;
+                    cur = (int)(c.x >> 8) - 1;
+                    m = c.x & 255u;
+                    sp = (int)(c.y & 255u);
+                    shadow = (c.y >> 8) & 1u;
+                    pend = (int)c.z;
+                    pend2 = (int)c.w;
+                    owner = o;
+                    my = stk0 + (o >> 6) * sstride + (o & 63);
+                    derive();
+                }
+            }
+        }
+        const bool busy = owner >= 0;
+        const unsigned long long bm = __builtin_amdgcn_ballot_w64(busy);
+        if (!bm) break;                 // nothing held, nothing claimed
+        if (trips == 0) nb0 = __builtin_popcountll(bm);
+        const float maxt = t;           // (any hit: t never changes; nearest: maxt unused)
+        if (busy && m != 0 && pend2 == 0) {
+            WALK_PROF(W, 1);
+            int cw;
+            if (cur < 0) {
+                cw = 0;
+                m = 0;
+            } else {
+                const int p = __builtin_ctz(m);
+                m &= m - 1;
+                cw = (int)Lw[cur * WIDE_WORDS + 8 + (p ^ oct)];
+            }
+            if (cw < 0) {
+                if (pend == 0) pend = ~cw;
+                else pend2 = ~cw;
+            } else {
+                ray3 rr;
+                rr.o = ro;
+                rr.d = rd;
+                const unsigned hm = wide_visit(L + 7 * cw, rr, ix, iy, iz, alpha, oct, shadow ? maxt : t);
+                if (hm) {
+                    if (m) {
+                        my[64 * sp] = ((unsigned)cur << 8) | m;
+                        sp++;
+                    }
+                    cur = cw;
+                    m = hm;
+                }
+            }
+            if (m == 0 && sp > 0) {
+                sp--;
+                const unsigned e2 = my[64 * sp];
+                cur = (int)(e2 >> 8);
+                m = e2 & 255u;
+            }
+        }
+        trips++;
+        const unsigned long long pm = __builtin_amdgcn_ballot_w64(busy && pend != 0);
+        const unsigned long long sm = __builtin_amdgcn_ballot_w64(busy && m != 0 && pend2 == 0);
+        // (refill > 64: claims at the call's start only, then wide_walk's stop rule)
+        const bool out = trips >= budget || ((dry || refill > 64) && 64 * __builtin_popcountll(pm | sm) <= stop * (refill > 64 ? nb0 : n0));
+        const bool leaves = pm != 0 && (sm == 0 || out || 64 * __builtin_popcountll(pm & ~sm) >= batch * __builtin_popcountll(pm | sm));
+        if (leaves && busy && pend != 0) {
+            WALK_PROF(W, 2);
+            const int f = pend & 0xffffff, c = pend >> 24, c4 = c < BVH_LEAF_MAX ? c : BVH_LEAF_MAX;
+            float4 g[BVH_LEAF_MAX];
+#pragma unroll
+            for (int q = 0; q < BVH_LEAF_MAX; q++) g[q] = B.geo[f + (q < c4 ? q : 0)];
+            float dq[BVH_LEAF_MAX];
+            bool bad = false;
+#pragma unroll
+            for (int q = 0; q < BVH_LEAF_MAX; q++) {
+                const float opx = g[q].x - ro.x, opy = g[q].y - ro.y, opz = g[q].z - ro.z;
+                const float bb = opx * rd.x + opy * rd.y + opz * rd.z;
+                const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g[q].w;
+                bad = bad || (q < c4 && fabsf(det) < 0x1p-96f);
+                const float sd = sqrt_nr(det);
+                const float t1 = bb - sd, t2 = bb + sd;
+                dq[q] = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
+            }
+            if (wave_any(bad)) {
+                ray3 rr;
+                rr.o = ro;
+                rr.d = rd;
+#pragma unroll
+                for (int q = 0; q < BVH_LEAF_MAX; q++) dq[q] = sphere_hit(g[q], rr);
+            }
+#pragma unroll
+            for (int q = 0; q < BVH_LEAF_MAX; q++) {
+                if (q < c4) {
+                    const float d = dq[q];
+                    if (shadow) {
+                        if (d < maxt) bpos = f + q;
+                    } else if (d < t) {
+                        t = d;
+                        bpos = f + q;
+                    } else if (d == t) {
+                        const int cur_id = bpos >= 0 ? B.id[bpos] : id;
+                        if (B.id[f + q] > cur_id) bpos = f + q;
+                    }
+                }
+            }
+            if (c > BVH_LEAF_MAX) {
+                pend = (f + BVH_LEAF_MAX) | ((c - BVH_LEAF_MAX) << 24);
+            } else {
+                pend = pend2;
+                pend2 = 0;
+            }
+            if (shadow && (id >= 0 || bpos >= 0)) {
+                m = 0;
+                sp = 0;
+                pend = pend2 = 0;
+            }
+        }
+        // ---- finished walks: the result to the owner's slot, the lane idle
+        if (busy && m == 0 && pend == 0) {
+            if (bpos >= 0) id = shadow ? 0x7fffffff : B.id[bpos];
+            P.res[owner] = make_uint2(__float_as_uint(t), (unsigned)id);
+            owner = -1;
+        }
+        if (out) break;
+    }
+    // ---- walks still held go back to the pool
+    if (owner >= 0) {
+        P.p0[owner] = make_uint4(__float_as_uint(ro.x), __float_as_uint(ro.y), __float_as_uint(ro.z), __float_as_uint(t));
+        P.p1[owner] = make_uint4(__float_as_uint(rd.x), __float_as_uint(rd.y), __float_as_uint(rd.z), (unsigned)id);
+        P.p2[owner] = make_uint4(((unsigned)(cur + 1) << 8) | m, (unsigned)sp | (shadow ? 256u : 0u), (unsigned)pend,
+                                 (unsigned)pend2);
+        P.pb[owner] = bpos;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __hip_atomic_fetch_or(P.bits + (owner >> 5), 1u << (owner & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_or(P.bits + 32, 1u << (owner >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Cooperative 8-wide walk: EIGHT lanes per ray (the heaviest tiles).
 //
 // A heavy tile's critical path is one pixel's 64-sample RNG chain of ~900
@@ -1282,8 +1565,12 @@ constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2, GEO_WIDE = 3;
 #ifndef RT_WIDE_SPREAD
 #define RT_WIDE_SPREAD 1    // 8-wide persistent kernels: first tier-1 sub-items assigned wave-major (A/B: 0)
 #endif
+#ifndef RT_WIDE_POOL
+#define RT_WIDE_POOL 0      // uncounted 8-wide kernels: the block pool of parked walks (wide_walk_pool; A/B:
+                            // exact, configs[4] 24.3 -> 32.8 ms at its best setting, profiles/r05/c4_walk_pool_ab.log)
+#endif
 #ifndef RT_SPT_REFILL
-#define RT_SPT_REFILL 0     // 8-wide persistent kernels: a lane whose pixel is done takes the next pixel (A/B: 1;
+#define RT_SPT_REFILL 0    // 8-wide persistent kernels: a lane whose pixel is done takes the next pixel (A/B: 1;
                             // 2: not in waves that started on a routed heavy tile)
 #endif
 #ifndef RT_SPT_REFILL_BATCH
@@ -1352,6 +1639,13 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // block its lanes' stacks ((wdepth - 1) entries x 64 lanes x 4 B).
     const uint4 *wL = (const uint4 *)smem;
     unsigned *wstk = nullptr;
+    // RT_WIDE_POOL (uncounted kernels, sflags bit 1): the block's pool of
+    // parked walks (wide_walk_pool) after the stacks.
+    constexpr bool POOLED = GEO == GEO_WIDE && !COUNT && RT_WIDE_POOL;
+    const int wsstride = 64 * (bvh.wdepth > 1 ? bvh.wdepth - 1 : 1);
+    WidePool wpool = {};
+    if (POOLED)
+        wpool = pool_carve(smem + (size_t)112 * bvh.wnodes + (size_t)(blockDim.x >> 6) * 4 * wsstride);
     if (GEO == GEO_WIDE) {
         uint4 *d = (uint4 *)smem;
         for (int i = threadIdx.x; i < 7 * bvh.wnodes; i += blockDim.x) d[i] = bvh.wnode[i];
@@ -1359,6 +1653,8 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             for (int i = threadIdx.x; i < 2 * bvh.wnodes; i += blockDim.x) d[7 * bvh.wnodes + i] = bvh.wmax[i];
         wstk = (unsigned *)(smem + (size_t)(COUNT ? 144 : 112) * bvh.wnodes) +
                (size_t)(threadIdx.x >> 6) * 64 * (bvh.wdepth - 1);
+        if (POOLED && (sflags & 2))
+            for (int i = threadIdx.x; i < 33; i += blockDim.x) wpool.bits[i] = 0u;
         __syncthreads();
     }
 
@@ -1747,9 +2043,42 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 const unsigned long long tr_w0 = __builtin_amdgcn_s_memtime();
                 tr_queries += !walking;
 #endif
+                if (POOLED && (sflags & 2) && !coop) {
+                    // Pooled: a new query starts here (its origin and
+                    // direction kept in its slot, its result pending); a
+                    // lane whose query is parked works on the pool instead.
+                    const int me = threadIdx.x;
+                    if (!walking) {
+                        wide_begin<COUNT>(bvh, ray, shadow, t, walk);
+                        wpool.p0[me] = make_uint4(__float_as_uint(ray.o.x), __float_as_uint(ray.o.y),
+                                                  __float_as_uint(ray.o.z), 0u);
+                        wpool.p1[me] = make_uint4(__float_as_uint(ray.d.x), __float_as_uint(ray.d.y),
+                                                  __float_as_uint(ray.d.z), 0u);
+                        wpool.res[me] = make_uint2(0u, (unsigned)POOL_SENT);
+                    }
+                    wide_walk_pool(bvh, wL, (unsigned *)(smem + (size_t)112 * bvh.wnodes), wsstride, wpool, !walking,
+                                   ray, shadow, walk, split, (sflags >> 8) & 255);
+                    // (the ray comes back from the slot on every path, so
+                    // it is not held in registers across the call)
+                    const uint2 rr = wpool.res[me];
+                    const uint4 a = wpool.p0[me], b = wpool.p1[me];
+                    ray.o = mk(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z));
+                    ray.d = mk(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z));
+                    walking = (int)rr.y == POOL_SENT;
+#ifdef RT_SPT_TRACE
+                    tr_walk += (unsigned)(__builtin_amdgcn_s_memtime() - tr_w0);
+#endif
+                    if (walking) continue;
+                    SPT_PROF(PB_WSHADE);
+                    t = __uint_as_float(rr.x);
+                    id = (int)rr.y;
+                    first = id;
+                } else {
                 if (!walking) wide_begin<COUNT>(bvh, ray, shadow, t, walk);
+                // (pooled builds: only the cooperative walk here -- the host
+                // launches them with the pool on)
                 walking = coop ? !wide_walk_coop<COUNT, RT_SPT_COOP_G>(bvh, wL, wstk, ray, shadow, walk, split)
-                               : !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
+                        : POOLED ? false : !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
 #ifdef RT_SPT_TRACE
                 tr_walk += (unsigned)(__builtin_amdgcn_s_memtime() - tr_w0);
 #endif
@@ -1758,6 +2087,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 t = walk.t;
                 id = walk.id;
                 first = id;                 // any hit: the highest occluder (COUNT)
+                }
             } else {
 #if RT_SPT_QV == 2
                 id = query_bf<COUNT>(geo, ray, t, first);
@@ -2373,8 +2703,20 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
     if (GEO == rt::smallpt::GEO_BVH && RT_SPT_GSTORE) lds = (size_t)(g.wpb / 4) * rt::smallpt::GS_BYTES;
     if (g.wpb == 16 && lds < 81 * 1024) lds = 81 * 1024;   // > half the CU's 160 KiB: one block per CU
     int *work = nullptr;
+    int sflags = (sc.no_refr && !getenv("RT_SPT_FULL_PASSA")) ? 1 : 0;   // (env: A/B)
     if (GEO == rt::smallpt::GEO_WIDE) {
         lds = wide_lds_bytes(sc.bvh.wnodes, sc.bvh.wdepth, g.wpb, COUNT);
+        // The block pool of parked walks (RT_WIDE_POOL builds, uncounted
+        // kernels) when it fits beside the nodes and stacks; RT_SPT_POOL=0
+        // turns it off, RT_SPT_POOL=k sets the claim threshold (k/64 idle).
+        if (RT_WIDE_POOL && !COUNT && lds + rt::smallpt::pool_bytes() <= 160 * 1024) {
+            const char *e = getenv("RT_SPT_POOL");
+            const int refill = e ? atoi(e) : RT_WIDE_POOL_REFILL;
+            if (refill > 0) {
+                lds += rt::smallpt::pool_bytes();
+                sflags |= 2 | (std::min(refill, 65) << 8);
+            }
+        }
         if (!(work = work_entry(sc, s))) return rtrt::check_launch("spt work counters") ? RT_ERR_HIP : RT_ERR_INVALID;
     }
     // Heavy tiles (with a learnt order, GEO_WIDE persistent launches), in
@@ -2422,7 +2764,7 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
     hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.nslots, g.gstride, first,
                        ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt, work, split,
-                       nheavy, (sc.no_refr && !getenv("RT_SPT_FULL_PASSA")) ? 1 : 0);   // (env: A/B)
+                       nheavy, sflags);
     return RT_OK;
 }
 
