@@ -1573,6 +1573,10 @@ constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2, GEO_WIDE = 3;
 #define RT_SPT_REFILL 0    // 8-wide persistent kernels: a lane whose pixel is done takes the next pixel (A/B: 1;
                             // 2: not in waves that started on a routed heavy tile)
 #endif
+#ifndef RT_SPT_REFILL_COUNT
+#define RT_SPT_REFILL_COUNT 1   // ... and in the full-counter 8-wide kernel (configs[4] counted 60-61 -> 51 ms: its
+                                // highest-occluder shadow walks spread a tile's pixel durations; A/B: 0)
+#endif
 #ifndef RT_SPT_REFILL_BATCH
 #define RT_SPT_REFILL_BATCH 1   // refill once this many lanes are free (or no lane of the wave has a pixel)
 #endif
@@ -1775,7 +1779,11 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // beside the fractal): waiting for the tile's slowest pixel left 28 % of
     // the lanes idle (tools/c4_lanes.py).  Every pixel's computation is
     // unchanged -- only which lane runs it, and when.
-    const bool refill = RT_SPT_REFILL && PERSIST && !heavy_ && (RT_SPT_REFILL == 1 || f >= (n1 << hs) + n2);
+    // (The counted kernel refills by default: there the tile tail, not the
+    // levelling, dominates -- 28 of 64 lanes per iteration without refill,
+    // 52 with, profiles/r05/c4_counted_refill.log.)
+    constexpr int REFILL = (COUNT && RT_SPT_REFILL_COUNT && !RT_SPT_REFILL) ? 1 : RT_SPT_REFILL;
+    const bool refill = REFILL && PERSIST && !heavy_ && (REFILL == 1 || f >= (n1 << hs) + n2);
 #ifdef RT_SPT_TRACE
     bool active = gvalid && lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end &&
                   (g_spt_only_group < 0 || grp == g_spt_only_group);

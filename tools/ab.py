@@ -3,7 +3,7 @@ process per variant, interleaved rounds, HIP-event time on the launch stream).
 
     KERNEL=smallpt|whitted LIBS=a,b ROUNDS=2 REPS=5 python tools/ab.py
 
-smallpt: Cornell 1920x1080, SPP (default 64) samples per launch; BAND=k/N renders
+smallpt: Cornell 1920x1080, SPP (default 64) samples per launch (COUNT=full|rays: with counters); BAND=k/N renders
 only row band k of N (rtamd.dist.row_band: the per-GPU work of an N-GPU frame).
 whitted: raytracer3.0.06 scene, 1920x1080 (WH=640x480: configs[0]'s size), rows [20, H-70).
 """
@@ -31,7 +31,7 @@ def child():
         d_prims.copy_(torch.frombuffer(bytearray(prims), dtype=torch.uint8))
         px = torch.zeros(W * H, dtype=torch.int32, device=dev)
 
-        def run():
+        def run(warm=False):
             rtamd.check(L.rtw_render_async(d_prims.data_ptr(), n, px.data_ptr(), W, H, 20, H - 70, None,
                                            st.cuda_stream))
     else:
@@ -53,19 +53,26 @@ def child():
         col = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
         px = torch.zeros(W * H, dtype=torch.int32, device=dev)
         grp = os.environ.get("GROUP")              # k/N: the interleaved share of rank k of N
+        # COUNT=full: all four counters (the counted kernel); COUNT=rays: calls and samples only
+        cmode = os.environ.get("COUNT", "")
+        cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+        cm = {"cptr": cnt.data_ptr() if cmode else None,
+              "mode": rtamd.SPT_PATH_TRACING | (rtamd.SPT_COUNT_RAYS if cmode == "rays" else 0)}
+        plain = os.environ.get("WARM_PLAIN")       # warm-up launches uncounted (they learn the tile order)
 
-        def run():
+        def run(warm=False):
+            mode, cptr = (0, None) if (warm and plain) else (cm["mode"], cm["cptr"])
             if grp:
                 k, N = (int(v) for v in grp.split("/"))
                 rtamd.check(L.spt_scene_render_groups_async(sc.handle, C.byref(cam), col.data_ptr(),
                                                             seeds0.data_ptr(), seeds.data_ptr(), px.data_ptr(),
-                                                            W, H, k, N, 0, SPP, 0, None, st.cuda_stream))
+                                                            W, H, k, N, 0, SPP, mode, cptr, st.cuda_stream))
                 return
             rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
-                                                 seeds.data_ptr(), px.data_ptr(), W, H, r0, r1, 0, SPP, 0,
-                                                 None, st.cuda_stream))
+                                                 seeds.data_ptr(), px.data_ptr(), W, H, r0, r1, 0, SPP, mode,
+                                                 cptr, st.cuda_stream))
     for _ in range(int(os.environ.get("WARM", "3" if os.environ.get("SCENE") == "c4" else "1"))):
-        run()
+        run(warm=True)
     torch.cuda.synchronize()
     ts = []
     for _ in range(int(os.environ.get("REPS", "5"))):
