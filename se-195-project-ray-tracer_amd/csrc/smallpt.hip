@@ -2578,6 +2578,7 @@ struct spt_scene {
     std::vector<rt_sphere> host;
     bool force_global = false;        // RT_SPT_GEO=global: scalar-load path at any size (A/B)
     mutable SptSched sched;           // adaptive group order (hierarchy scenes)
+    mutable SptSched sched_cnt;       //   ... of the full-counter launches (their own tile costs)
     // Work counters of the persistent (8-wide hierarchy) launches: a ring,
     // one zeroed quad (rest, routed heavy, cooperative, unused) per launch, so
     // launches in flight on several streams do not share one.
@@ -2974,13 +2975,15 @@ extern "C" int spt_scene_destroy(spt_scene *sc)
     if (sc->d_soa) (void)hipFree(sc->d_soa);
     if (sc->d_bvh) (void)hipFree(sc->d_bvh);
     if (sc->d_work) (void)hipFree(sc->d_work);
-    SptSched &q = sc->sched;
-    if (q.d_cost) (void)hipFree(q.d_cost);
-    if (q.d_order) (void)hipFree(q.d_order);
-    for (int *p : q.retired) (void)hipFree(p);
-    if (q.h_cost) (void)hipHostFree(q.h_cost);
-    if (q.h_order) (void)hipHostFree(q.h_order);
-    if (q.ev) (void)hipEventDestroy(q.ev);
+    for (SptSched *qp : {&sc->sched, &sc->sched_cnt}) {
+        SptSched &q = *qp;
+        if (q.d_cost) (void)hipFree(q.d_cost);
+        if (q.d_order) (void)hipFree(q.d_order);
+        for (int *p : q.retired) (void)hipFree(p);
+        if (q.h_cost) (void)hipHostFree(q.h_cost);
+        if (q.h_order) (void)hipHostFree(q.h_order);
+        if (q.ev) (void)hipEventDestroy(q.ev);
+    }
     delete sc;
     return RT_OK;
 }
@@ -3001,7 +3004,13 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
 {
     const char *e = getenv("RT_SPT_SCHED");
     if (!sc.bvh.node || (e && atoi(e) == 0)) return false;   // the full-scan kernels have no order/cost code
-    SptSched &q = sc.sched;
+    // Full-counter launches learn and use an order of their own: their
+    // shadow walks seek the highest-index occluder (twice the uncounted
+    // walk's work, unevenly over the tiles), so their tile costs would order
+    // the uncounted launches wrongly (configs[4]: 28.0 ms with such an order,
+    // 25.4 ms with the uncounted kernel's own) -- and the uncounted order is
+    // not theirs either (counted 44.7 ms with it, 52.9 ms with none).
+    SptSched &q = full_count ? sc.sched_cnt : sc.sched;
     const int nslots = g.nslots;
     if (!(q.w == w && q.h == h && q.r0 == r0 && q.r1 == r1 && q.gstride == gstride && q.ns == ns &&
           q.mode == mode && q.nslots == nslots && memcmp(&q.cam, &cam, sizeof(cam)) == 0)) {
@@ -3070,12 +3079,7 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
         g.heavy16 = std::min(std::max((heavy + 15) / 16, 0), 255);
         return false;
     }
-    // A full-counter launch does not record: its shadow walks look for the
-    // highest-index occluder (twice the uncounted walk's work, unevenly
-    // over the tiles), so its tile costs would order the uncounted launches
-    // wrongly (configs[4]: 28.0 ms with such an order, 25.4 ms with the
-    // uncounted kernel's own).
-    if (q.state == 0 && !full_count) {
+    if (q.state == 0) {
         if (hipMemsetAsync(q.d_cost, 0, sizeof(unsigned) * nslots, s) != hipSuccess) return false;
         g.cost = q.d_cost;
         return true;
@@ -3083,9 +3087,9 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
     return false;                                       // state 1, read-back in flight: plain launch
 }
 
-void sched_after(const spt_scene &sc, hipStream_t s)
+void sched_after(const spt_scene &sc, hipStream_t s, bool full_count)
 {
-    SptSched &q = sc.sched;
+    SptSched &q = full_count ? sc.sched_cnt : sc.sched;
     if (hipMemcpyAsync(q.h_cost, q.d_cost, sizeof(unsigned) * q.nslots, hipMemcpyDeviceToHost, s) == hipSuccess &&
         hipEventRecord(q.ev, s) == hipSuccess)
         q.state = 1;
@@ -3139,7 +3143,7 @@ int scene_render(const spt_scene *sc, const rt_camera *camera, float *d_colors, 
                                                   d_seeds_out, d_pixels, w, h, row_begin, row_end, first_sample,
                                                   nsamples, cnt);
     if (rc == RT_OK) rc = rtrt::check_launch("spt render_kernel");
-    if (rc == RT_OK && record) sched_after(*sc, s);
+    if (rc == RT_OK && record) sched_after(*sc, s, cmode == CNT_FULL);
     return rc;
 }
 }  // namespace

@@ -184,8 +184,9 @@ def test_configs4_cooperative_walk_golden(rt, oracle, counted, coop, monkeypatch
     first = None
     for i in range(3):
         f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n, camera=cam)
-        # (full-counter launches never record tile costs: an uncounted frame
-        # first, so the counted frames after it run the learnt order)
+        # (full-counter launches learn an order of their own: after the
+        # uncounted 1st frame, the 2nd records the counted tile costs and the
+        # 3rd runs the counted order, cooperative tiles included)
         f.render(64, counters=counted and i > 0)
         got = (oracle.fnv1a64(f.colors), oracle.fnv1a64(f.pixels), oracle.fnv1a64(f.seeds))
         assert got == (g["colors"], g["pixels"], g["seeds"])
