@@ -668,6 +668,9 @@ __device__ __forceinline__ unsigned wide_visit(const uint4 *__restrict__ N, cons
     return hm;
 }
 
+#ifndef RT_SPT_COOP_LEAN
+#define RT_SPT_COOP_LEAN 1  // cooperative walk: one trip as straight-line selects (N = 8 shares 10.1-10.4 -> 9.9-10.0 ms; A/B: 0)
+#endif
 #ifndef RT_SPT_COOP_NL
 #define RT_SPT_COOP_NL 2    // cooperative walk: leaves tested per pass (loads in flight together)
 #endif
@@ -1397,6 +1400,75 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
     const int pos = threadIdx.x & (G - 1), gbase = threadIdx.x & (64 - G);
     const int n0 = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true));
     int trips = 0;
+#if RT_SPT_COOP_LEAN
+    // One trip as straight-line selects: the next child's word and the
+    // stack top are read together at the trip's start (the pop can only
+    // need the entry below the current top: a trip that descends does not
+    // pop), every group's lanes run the visit (a group with nothing to visit
+    // masks its result), and only the leaf passes sit behind a wave-uniform
+    // branch.  The old form's per-group branches cost the lone heavy wave
+    // ~40 exec-mask and branch instructions per trip (c4_coop_phase_n8_spread.log).
+    while (true) {
+        const bool has = m != 0;
+        const int p = __builtin_ctz(m | 256u);
+        const unsigned mr = cur < 0 ? 0u : (m & (m - 1u));
+        const int cwl = (int)Lw[max(cur, 0) * WIDE_WORDS + 8 + ((p & 7) ^ oct)];
+        const unsigned e2 = my[64 * max(sp - 1, 0)];
+        const int cw = cur < 0 ? 0 : cwl;
+        bool occl = false;
+        const bool rootleaf = has && cw < 0;    // (a root leaf: child leaves are tested at their parent)
+        if (wave_any(rootleaf)) {
+            if (rootleaf) {
+                const int lf = ~cw;
+                const int fa[1] = {lf & 0xffffff}, ca[1] = {lf >> 24};
+                occl = leaf_coop<COUNT, G, 1>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id);
+            }
+        }
+        const bool vis = has && cw >= 0;
+        const int cv = vis ? cw : 0;
+        unsigned lm;
+        unsigned hm = COUNT ? wide_visit_coop<G>(L + 7 * cv, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase,
+                                                 lm, Lmax + 8 * cv, shadow ? id : -1)
+                            : wide_visit_coop<G>(L + 7 * cv, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase,
+                                                 lm);
+        hm = vis ? hm : 0u;
+        lm = vis ? lm : 0u;
+        if (wave_any(lm != 0)) {
+            unsigned l = lm;
+            while (l) {
+                int fa[RT_SPT_COOP_NL], ca[RT_SPT_COOP_NL];
+#pragma unroll
+                for (int q = 0; q < RT_SPT_COOP_NL; q++) {
+                    fa[q] = ca[q] = 0;
+                    if (l) {
+                        const int iq = __builtin_ctz(l);
+                        l &= l - 1;
+                        const int wq = ~(int)Lw[cv * WIDE_WORDS + 8 + (iq ^ oct)];
+                        fa[q] = wq & 0xffffff;
+                        ca[q] = wq >> 24;
+                    }
+                }
+                if (leaf_coop<COUNT, G, RT_SPT_COOP_NL>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id)) {
+                    occl = true;
+                    break;
+                }
+            }
+        }
+        const unsigned nm = hm & ~lm;
+        const bool desc = vis && nm != 0 && !occl;
+        if (desc && mr != 0) my[64 * sp] = ((unsigned)cur << 8) | mr;
+        sp = occl ? 0 : sp + ((desc && mr != 0) ? 1 : 0);
+        cur = desc ? cw : cur;
+        m = occl ? 0u : (desc ? nm : mr);
+        const bool pop = m == 0 && sp > 0;      // (then no push this trip: e2 is the top)
+        sp -= pop ? 1 : 0;
+        cur = pop ? (int)(e2 >> 8) : cur;
+        m = pop ? (e2 & 255u) : m;
+        trips++;
+        const unsigned long long am = __builtin_amdgcn_ballot_w64(m != 0);
+        if (am == 0 || trips >= budget || 64 * __builtin_popcountll(am) <= stop * n0) break;
+    }
+#else
     while (true) {
         if (m != 0) {
             int cw;
@@ -1478,6 +1550,7 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
         const unsigned long long am = __builtin_amdgcn_ballot_w64(m != 0);
         if (am == 0 || trips >= budget || 64 * __builtin_popcountll(am) <= stop * n0) break;
     }
+#endif
 #ifdef RT_SPT_TRACE
     W.tr_trips += trips;
 #endif
