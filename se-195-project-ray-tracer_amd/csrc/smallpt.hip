@@ -1434,6 +1434,10 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
         hm = vis ? hm : 0u;
         lm = vis ? lm : 0u;
         if (wave_any(lm != 0)) {
+#ifdef RT_SPT_TRACE
+            const unsigned long long tr_l0 = __builtin_amdgcn_s_memtime();
+            W.tr_leafruns++;
+#endif
             unsigned l = lm;
             while (l) {
                 int fa[RT_SPT_COOP_NL], ca[RT_SPT_COOP_NL];
@@ -1453,6 +1457,9 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
                     break;
                 }
             }
+#ifdef RT_SPT_TRACE
+            W.tr_leaf += (unsigned)(__builtin_amdgcn_s_memtime() - tr_l0);
+#endif
         }
         const unsigned nm = hm & ~lm;
         const bool desc = vis && nm != 0 && !occl;
