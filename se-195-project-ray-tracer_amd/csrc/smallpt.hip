@@ -671,6 +671,10 @@ __device__ __forceinline__ unsigned wide_visit(const uint4 *__restrict__ N, cons
 #ifndef RT_SPT_COOP_LEAN
 #define RT_SPT_COOP_LEAN 1  // cooperative walk: one trip as straight-line selects (N = 8 shares 10.1-10.4 -> 9.9-10.0 ms; A/B: 0)
 #endif
+#ifndef RT_SPT_COOP_LOCAL
+#define RT_SPT_COOP_LOCAL 1 // lean cooperative trip: nearest-hit bests kept per lane, reduced per leaf section
+                            // and per query instead of per leaf (N = 8 / 4 shares -2 to -3 %; A/B: 0)
+#endif
 #ifndef RT_SPT_COOP_NL
 #define RT_SPT_COOP_NL 2    // cooperative walk: leaves tested per pass (loads in flight together)
 #endif
@@ -1332,7 +1336,12 @@ __device__ __forceinline__ bool leaf_apply(const BvhView &B, bool shadow, float 
 // them are issued before the first test (one memory latency per pass), the
 // leaves then applied in order.  Returns true when an uncounted any-hit
 // found an occluder.
-template <bool COUNT, int G, int NL>
+// LOCAL (nearest hit): each lane keeps its own best (t, bpos) over the
+// spheres it tests -- no group reduction per leaf; wide_walk_coop reduces the
+// lanes' bests to the group's culling limit once per leaf section and to the
+// result once per query (the minimum with ties to the highest index: the
+// same choice, made once).
+template <bool COUNT, int G, int NL, bool LOCAL = false>
 __device__ __forceinline__ bool leaf_coop(const BvhView &B, const ray3 &r, bool shadow, float maxt,
                                           const int (&f)[NL], const int (&c)[NL], int pos, int gbase, float &t,
                                           int &bpos, int &id)
@@ -1372,7 +1381,21 @@ __device__ __forceinline__ bool leaf_coop(const BvhView &B, const ray3 &r, bool 
 #pragma unroll
             for (int j = 0; j < S; j++)
                 if (b + pos + j * G >= c[l]) d[j] = MISS;
-            if (leaf_apply<COUNT, G>(B, shadow, maxt, f[l], b, pos, gbase, d, t, bpos, id)) return true;
+            if (LOCAL && !shadow) {
+#pragma unroll
+                for (int j = 0; j < S; j++) {
+                    const int q = f[l] + b + pos + j * G;
+                    if (d[j] < t) {
+                        t = d[j];
+                        bpos = q;
+                    } else if (d[j] == t) {             // (d finite: a tie)
+                        const int cur_id = bpos >= 0 ? B.id[bpos] : id;
+                        if (B.id[q] > cur_id) bpos = q;
+                    }
+                }
+            } else if (leaf_apply<COUNT, G>(B, shadow, maxt, f[l], b, pos, gbase, d, t, bpos, id)) {
+                return true;
+            }
         }
     }
     return false;
@@ -1408,6 +1431,10 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
     // masks its result), and only the leaf passes sit behind a wave-uniform
     // branch.  The old form's per-group branches cost the lone heavy wave
     // ~40 exec-mask and branch instructions per trip (c4_coop_phase_n8_spread.log).
+    // (RT_SPT_COOP_LOCAL, nearest hits: t / bpos are the lane's own best;
+    // tg, the group's minimum, is the culling limit)
+    constexpr bool LOC = G == 8 && RT_SPT_COOP_LOCAL;
+    float tg = LOC ? grp_min<G>(t) : t;
     while (true) {
         const bool has = m != 0;
         const int p = __builtin_ctz(m | 256u);
@@ -1421,15 +1448,16 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
             if (rootleaf) {
                 const int lf = ~cw;
                 const int fa[1] = {lf & 0xffffff}, ca[1] = {lf >> 24};
-                occl = leaf_coop<COUNT, G, 1>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id);
+                occl = leaf_coop<COUNT, G, 1, LOC>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id);
             }
+            if (LOC) tg = grp_min<G>(t);
         }
         const bool vis = has && cw >= 0;
         const int cv = vis ? cw : 0;
         unsigned lm;
-        unsigned hm = COUNT ? wide_visit_coop<G>(L + 7 * cv, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase,
+        unsigned hm = COUNT ? wide_visit_coop<G>(L + 7 * cv, r, ix, iy, iz, alpha, oct, shadow ? maxt : (LOC ? tg : t), pos, gbase,
                                                  lm, Lmax + 8 * cv, shadow ? id : -1)
-                            : wide_visit_coop<G>(L + 7 * cv, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase,
+                            : wide_visit_coop<G>(L + 7 * cv, r, ix, iy, iz, alpha, oct, shadow ? maxt : (LOC ? tg : t), pos, gbase,
                                                  lm);
         hm = vis ? hm : 0u;
         lm = vis ? lm : 0u;
@@ -1452,11 +1480,12 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
                         ca[q] = wq >> 24;
                     }
                 }
-                if (leaf_coop<COUNT, G, RT_SPT_COOP_NL>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id)) {
+                if (leaf_coop<COUNT, G, RT_SPT_COOP_NL, LOC>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id)) {
                     occl = true;
                     break;
                 }
             }
+            if (LOC) tg = grp_min<G>(t);
 #ifdef RT_SPT_TRACE
             W.tr_leaf += (unsigned)(__builtin_amdgcn_s_memtime() - tr_l0);
 #endif
@@ -1556,6 +1585,24 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
         trips++;
         const unsigned long long am = __builtin_amdgcn_ballot_w64(m != 0);
         if (am == 0 || trips >= budget || 64 * __builtin_popcountll(am) <= stop * n0) break;
+    }
+#endif
+#if RT_SPT_COOP_LEAN
+    if (LOC && m == 0 && !shadow) {
+        // the group's result from its lanes' bests: the minimum distance,
+        // ties to the highest reference index (bpos -1: the query's first id)
+        const float tf = grp_min<G>(t);
+        const bool cand = t == tf;
+        int wb;
+        if (__builtin_popcount(grp_bits<G>(cand, gbase)) <= 1) {
+            wb = grp_max<G>(cand ? bpos : -1);
+        } else {
+            const int cid = cand ? (bpos >= 0 ? B.id[bpos] : id) : (int)0x80000000;
+            const int im = grp_max<G>(cid);
+            wb = grp_max<G>((cand && cid == im) ? bpos : -1);
+        }
+        t = tf;
+        bpos = wb;
     }
 #endif
 #ifdef RT_SPT_TRACE
