@@ -489,24 +489,29 @@ def list_tiled_line(dev, rank, world, distributed, s, sc, cm, spp, workload, fra
     cnt = torch.zeros(4, dtype=torch.int64, device=dev)
     cost = torch.zeros(ng, dtype=torch.int32, device=dev)
 
-    def render(lst, b, counters=None, cost_buf=None):
+    def render(lst, b, counters=None, cost_buf=None, flags=0):
         rtamd.check(L.spt_scene_render_list_async(
             sc.handle, C.byref(cm), cols[b].data_ptr(), seeds0.data_ptr(), seeds.data_ptr(), pxs[b].data_ptr(),
-            W, H, lst.data_ptr(), lst.numel(), 0, spp, rtamd.SPT_PATH_TRACING | rtamd.SPT_COUNT_RAYS,
+            W, H, lst.data_ptr(), lst.numel(), 0, spp, rtamd.SPT_PATH_TRACING | rtamd.SPT_COUNT_RAYS | flags,
             counters.data_ptr() if counters is not None else None,
             cost_buf.data_ptr() if cost_buf is not None else None, s.cuda_stream))
 
     mine0 = torch.tensor(rdist.interleaved_groups(rank, world, W, H), dtype=torch.int32, device=dev)
     render(mine0, 0, counters=cnt, cost_buf=cost)            # learning frame: costs + rays (rays-only mode)
+    cost_max = torch.zeros_like(cost)                        # and each group's longest tile (the order key)
+    render(mine0, 1, cost_buf=cost_max, flags=rtamd.SPT_COST_MAX)
     torch.cuda.synchronize(dev)
     costs = cost.to(torch.int64)
+    keys = cost_max.to(torch.int64)
     counts = cnt.clone()
     if distributed:
         dist.all_reduce(costs)
+        dist.all_reduce(keys)                                # (one rank renders each group: a sum is its value)
         dist.all_reduce(counts)
     costs = costs.cpu().numpy()
+    keys = keys.cpu().numpy()
     counts = counts.tolist()
-    parts = rdist.balanced_partition(costs, world)
+    parts = rdist.balanced_partition(costs, world, order_key=keys)
     mine = torch.tensor(parts[rank], dtype=torch.int32, device=dev)
     gs = torch.cuda.Stream(dev)
 
@@ -576,7 +581,8 @@ def list_tiled_line(dev, rank, world, distributed, s, sc, cm, spp, workload, fra
                workload, world, collective_name()),
            "n_gpus": world, "ms_per_frame": round(ms, 3), "Mrays_per_s": round(rays / ms / 1e3, 2),
            "Msamples_per_s": round(W * H * spp / ms / 1e3, 2), "rays_per_frame": rays,
-           "partition": "rtamd.dist.balanced_partition over one learning frame's per-group wave times",
+           "partition": "rtamd.dist.balanced_partition over one learning frame's per-group wave times (balanced "
+                        "by their sum, each rank's list ordered by the group's longest tile: SPT_COST_MAX)",
            "render_ms_per_rank": per_rank,
            "predicted_load_per_rank": [int(costs[p].sum()) for p in parts]}
     # the assembled frame must equal one GPU rendering the whole frame

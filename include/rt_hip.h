@@ -142,6 +142,12 @@ int rtw_render_ocl_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xr
  * early-exit position (geomfunc.h:94-110: the highest-index occluder), which
  * costs hierarchy scenes a longer shadow walk; the call counts do not. */
 #define SPT_COUNT_RAYS 0x100
+/* Flag OR-ed into `mode` of spt_scene_render_list_async with d_group_cost:
+ * each listed group's entry receives the LONGEST of its tiles' wave times
+ * (atomic max) instead of their sum -- the length of the group's slowest
+ * pixel chain, the order key for the heavy-tile treatment (list such groups
+ * first), where the sum is the load to balance. */
+#define SPT_COST_MAX 0x200
 
 /* Blocking, host buffers, whole frame.  Runs samples first_sample ..
  * first_sample+nsamples-1 of every pixel, exactly as nsamples successive

@@ -2545,8 +2545,11 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         }
     }
 #undef GS_BASE
-    if (SCHED && group_cost && gvalid && lane == 0 && !refill)   // this tile's duration (100 MHz ticks), summed per group
-        atomicAdd(&group_cost[grp], (unsigned)(__builtin_amdgcn_s_memrealtime() - t_start));
+    if (SCHED && group_cost && gvalid && lane == 0 && !refill) {  // this tile's duration (100 MHz ticks), summed per group
+        const unsigned dur = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_start);
+        if (sflags & 4) atomicMax(&group_cost[grp], dur);           // (Shape::cost_max: the group's longest tile)
+        else atomicAdd(&group_cost[grp], dur);
+    }
 #ifdef RT_SPT_TRACE
     {
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
@@ -2756,6 +2759,7 @@ struct Shape {
     unsigned *cost = nullptr;
     int heavy16 = 0;                  // with order: heaviest slots kept at top priority, in 16s
     bool tiers = true;                // with order: its first tiles get the heavy-tile treatment
+    bool cost_max = false;            // cost: a group's longest tile (atomic max), not the sum
 };
 // Rows [r0, r1), or (gstride > 1) the 8-row groups r0/8, r0/8 + gstride, ...
 // below r1 (r0 a multiple of 8); or (nlist > 0) the nlist tile groups of a
@@ -2840,6 +2844,7 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
     if (g.wpb == 16 && lds < 81 * 1024) lds = 81 * 1024;   // > half the CU's 160 KiB: one block per CU
     int *work = nullptr;
     int sflags = (sc.no_refr && !getenv("RT_SPT_FULL_PASSA")) ? 1 : 0;   // (env: A/B)
+    if (g.cost_max) sflags |= 4;
     if (GEO == rt::smallpt::GEO_WIDE) {
         lds = wide_lds_bytes(sc.bvh.wnodes, sc.bvh.wdepth, g.wpb, COUNT);
         // The block pool of parked walks (RT_WIDE_POOL builds, uncounted
@@ -3030,7 +3035,7 @@ int check_render_args(const rt_camera *camera, float *d_colors, const uint32_t *
         return rtrt::fail(RT_ERR_INVALID, "spt render: bad sizes");
     if (row_begin < 0 || row_end > h || row_begin > row_end)
         return rtrt::fail(RT_ERR_INVALID, "spt render: bad row range");
-    const int base = mode & ~SPT_COUNT_RAYS;
+    const int base = mode & ~(SPT_COUNT_RAYS | SPT_COST_MAX);
     if (base != SPT_PATH_TRACING && base != SPT_DIRECT_LIGHTING)
         return rtrt::fail(RT_ERR_INVALID, "spt render: bad mode");
     return RT_OK;
@@ -3209,6 +3214,14 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
     if (q.state == 0) {
         if (hipMemsetAsync(q.d_cost, 0, sizeof(unsigned) * nslots, s) != hipSuccess) return false;
         g.cost = q.d_cost;
+        // The order key is a group's longest tile (its slowest pixel chain),
+        // not the sum of its four: the heavy-tile treatment (cooperative or
+        // routed tiles) goes to the first groups in order, and a group with
+        // one very long tile outranks four middling ones (configs[4] N = 4
+        // interleaved windows 17.1 -> 16.3 ms; the full frame level).
+        // RT_SPT_COST_MAX=0: the sum (A/B).
+        const char *cm = getenv("RT_SPT_COST_MAX");
+        g.cost_max = !(cm && atoi(cm) == 0);
         return true;
     }
     return false;                                       // state 1, read-back in flight: plain launch
@@ -3232,7 +3245,7 @@ int scene_render(const spt_scene *sc, const rt_camera *camera, float *d_colors, 
     if (row_begin >= row_end || (d_list && nlist < 1)) return RT_OK;
     Shape grid = launch_shape(*sc, w, row_begin, row_end, gstride, d_list ? nlist : 0);
     hipStream_t s = (hipStream_t)stream;
-    const int base = mode & ~SPT_COUNT_RAYS;
+    const int base = mode & ~(SPT_COUNT_RAYS | SPT_COST_MAX);
     bool record = false;
     if (d_list) {
         // The caller's order, heaviest first: its first groups get the
@@ -3242,6 +3255,7 @@ int scene_render(const spt_scene *sc, const rt_camera *camera, float *d_colors, 
         // a lane per pixel, so the recorded costs compare like with like.
         grid.order = d_list;
         grid.cost = sc->bvh.node ? d_cost : nullptr;
+        grid.cost_max = (mode & SPT_COST_MAX) != 0;
         grid.tiers = d_cost == nullptr;
         grid.heavy16 = 0;                 // (no group held at the top priority: see sched_before)
         if (const char *he = getenv("RT_SPT_HEAVY"))

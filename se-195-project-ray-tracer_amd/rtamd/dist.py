@@ -145,13 +145,16 @@ def interleaved_groups(rank, world, w, h):
     return [g for g in range(group_count(w, h)) if ((4 * g) // tx) % world == rank]
 
 
-def balanced_partition(costs, world):
+def balanced_partition(costs, world, order_key=None):
     """Deterministic longest-processing-time split of the groups over `world`
     ranks: groups in decreasing cost (ties: lower index first), each to the
     rank with the least total so far (ties: lower rank).  Returns per rank
     its groups in that order -- heaviest first, which is also the dispatch
-    order spt_scene_render_list_async wants.  Every rank computes the same
-    lists from the same (all-reduced) costs."""
+    order spt_scene_render_list_async wants -- or, with `order_key` (per
+    group, e.g. its longest tile: SPT_COST_MAX), each rank's groups sorted by
+    decreasing key (ties: lower index first), so the groups holding the
+    longest pixel chains take the list's heavy-tile slots.  Every rank
+    computes the same lists from the same (all-reduced) costs."""
     import heapq
     order = sorted(range(len(costs)), key=lambda g: (-int(costs[g]), g))
     heap = [(0, r) for r in range(world)]
@@ -160,6 +163,8 @@ def balanced_partition(costs, world):
         load, r = heapq.heappop(heap)
         parts[r].append(g)
         heapq.heappush(heap, (load + int(costs[g]), r))
+    if order_key is not None:
+        parts = [sorted(p, key=lambda g: (-int(order_key[g]), g)) for p in parts]
     return parts
 
 

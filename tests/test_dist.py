@@ -137,6 +137,24 @@ def test_balanced_partition_properties():
     assert rd.interleaved_groups(1, 4, 1920, 1080)[:3] == [60, 61, 62]
 
 
+def test_balanced_partition_order_key():
+    """order_key (a group's longest tile) reorders each rank's list by
+    decreasing key (ties: lower index) without changing which groups a rank
+    gets -- the loads stay balanced by the costs."""
+    import numpy as np
+    from rtamd import dist as rd
+    rng = np.random.default_rng(5)
+    costs = rng.integers(1, 1000, 4000)
+    keys = rng.integers(1, 300, 4000)
+    keys[rng.random(4000) < 0.5] = 7                       # many ties
+    for world in (1, 2, 4, 8):
+        plain = rd.balanced_partition(costs, world)
+        keyed = rd.balanced_partition(costs, world, order_key=keys)
+        for p, q in zip(plain, keyed):
+            assert sorted(p) == sorted(q)
+            assert all((-keys[a], a) < (-keys[b], b) for a, b in zip(q, q[1:]))
+
+
 def test_list_gather_refuses_overlapping_lists():
     """ListGather's lists must partition groups: a group in two ranks' lists
     (or twice in one), or outside the frame, is refused up front."""

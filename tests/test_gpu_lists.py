@@ -110,6 +110,22 @@ def test_list_costs_and_bad_arguments(rt):
     mask = np.zeros(ng, bool)
     mask[lst] = True
     assert (c[mask] > 0).all() and (c[~mask] == 0).all()
+    # SPT_COST_MAX: each listed group's longest tile instead of the sum of its
+    # (up to four) tiles -- between a quarter of the sum and the sum (the two
+    # frames' wave times differ a little: 10 % slack), the same frame
+    cmax = torch.zeros(ng, dtype=torch.int32, device=dev)
+    f2 = _Frame(torch, dev, w, h, seeds0)
+    rt.check(L.spt_scene_render_list_async(sc.handle, C.byref(cam), f2.col.data_ptr(), seeds0.data_ptr(),
+                                           f2.seeds.data_ptr(), f2.px.data_ptr(), w, h, d.data_ptr(), len(lst), 0, 2,
+                                           rt.SPT_COST_MAX, None, cmax.data_ptr(), st))
+    torch.cuda.synchronize()
+    m = cmax.cpu().numpy().astype(np.int64)
+    assert (m[mask] > 0).all() and (m[~mask] == 0).all()
+    assert (m[mask] <= 1.1 * c[mask]).all() and (m[mask] >= 0.9 * c[mask] / 4).all()
+    assert torch.equal(f2.col.view(torch.int32), f.col.view(torch.int32)) and torch.equal(f2.px, f.px)
+    assert L.spt_scene_render_list_async(sc.handle, C.byref(cam), f2.col.data_ptr(), seeds0.data_ptr(),
+                                         f2.seeds.data_ptr(), f2.px.data_ptr(), w, h, d.data_ptr(), len(lst), 0, 1,
+                                         0x400, None, None, st) == rt._lib.RT_ERR_INVALID
     big = torch.zeros(ng + 1, dtype=torch.int32, device=dev)
     assert L.spt_scene_render_list_async(sc.handle, C.byref(cam), f.col.data_ptr(), seeds0.data_ptr(),
                                          f.seeds.data_ptr(), f.px.data_ptr(), w, h, big.data_ptr(), ng + 1, 0, 1, 0,

@@ -56,10 +56,10 @@ def timed(fn):
     return float(np.median(ts)), min(ts)
 
 
-def render_list(sc, lst, col, sd, px, cost=None):
+def render_list(sc, lst, col, sd, px, cost=None, flags=0):
     rtamd.check(L.spt_scene_render_list_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
                                               sd.data_ptr(), px.data_ptr(), W, H, lst.data_ptr(), lst.numel(), 0,
-                                              SPP, 0, None, cost.data_ptr() if cost is not None else None,
+                                              SPP, flags, None, cost.data_ptr() if cost is not None else None,
                                               st.cuda_stream))
 
 
@@ -114,9 +114,13 @@ def main():
         cost.zero_()
         for k in range(N):
             render_list(sc, lists0[k], *out, cost=cost)
+        cmax = torch.zeros_like(cost)                            # each group's longest tile: the order key
+        for k in range(N):
+            render_list(sc, lists0[k], *bufs(), cost=cmax, flags=rtamd.SPT_COST_MAX)
         torch.cuda.synchronize()
         c = cost.cpu().numpy().astype(np.int64)
-        parts = rdist.balanced_partition(c, N)
+        parts = rdist.balanced_partition(c, N, order_key=None if os.environ.get("C4_SUM_ORDER") else
+                                         cmax.cpu().numpy().astype(np.int64))
         print("  learnt costs: total %d ticks, max group %d, predicted per-rank loads %s" % (
             c.sum(), c.max(), [int(c[p].sum()) for p in parts]), flush=True)
         # SWEEP="n1:hw,..." times the balanced lists under other heavy-tile
