@@ -102,17 +102,19 @@ def test_list_costs_and_bad_arguments(rt):
     lst = list(range(0, ng, 3))
     d = torch.tensor(lst, dtype=torch.int32, device=dev)
     cost = torch.zeros(ng, dtype=torch.int32, device=dev)
-    rt.check(L.spt_scene_render_list_async(sc.handle, C.byref(cam), f.col.data_ptr(), seeds0.data_ptr(),
-                                           f.seeds.data_ptr(), f.px.data_ptr(), w, h, d.data_ptr(), len(lst), 0, 2,
-                                           0, None, cost.data_ptr(), st))
+    for cbuf in (None, cost):                 # (a warm-up launch first: the timed ones compare)
+        rt.check(L.spt_scene_render_list_async(sc.handle, C.byref(cam), f.col.data_ptr(), seeds0.data_ptr(),
+                                               f.seeds.data_ptr(), f.px.data_ptr(), w, h, d.data_ptr(), len(lst), 0,
+                                               2, 0, None, cbuf.data_ptr() if cbuf is not None else None, st))
     torch.cuda.synchronize()
     c = cost.cpu().numpy()
     mask = np.zeros(ng, bool)
     mask[lst] = True
     assert (c[mask] > 0).all() and (c[~mask] == 0).all()
     # SPT_COST_MAX: each listed group's longest tile instead of the sum of its
-    # (up to four) tiles -- between a quarter of the sum and the sum (the two
-    # frames' wave times differ a little: 10 % slack), the same frame
+    # (up to four) tiles -- over all groups well below the sums and above a
+    # quarter of them (two launches' wave times, so only in aggregate); the
+    # same frame
     cmax = torch.zeros(ng, dtype=torch.int32, device=dev)
     f2 = _Frame(torch, dev, w, h, seeds0)
     rt.check(L.spt_scene_render_list_async(sc.handle, C.byref(cam), f2.col.data_ptr(), seeds0.data_ptr(),
@@ -121,7 +123,8 @@ def test_list_costs_and_bad_arguments(rt):
     torch.cuda.synchronize()
     m = cmax.cpu().numpy().astype(np.int64)
     assert (m[mask] > 0).all() and (m[~mask] == 0).all()
-    assert (m[mask] <= 1.1 * c[mask]).all() and (m[mask] >= 0.9 * c[mask] / 4).all()
+    ratio = m[mask].sum() / c[mask].sum()
+    assert 0.15 < ratio < 0.9, ratio
     assert torch.equal(f2.col.view(torch.int32), f.col.view(torch.int32)) and torch.equal(f2.px, f.px)
     assert L.spt_scene_render_list_async(sc.handle, C.byref(cam), f2.col.data_ptr(), seeds0.data_ptr(),
                                          f2.seeds.data_ptr(), f2.px.data_ptr(), w, h, d.data_ptr(), len(lst), 0, 1,
@@ -249,5 +252,5 @@ def test_count_rays_mode(rt, monkeypatch, kind, env):
         ca, cb = a.cnt.tolist(), b.cnt.tolist()
         assert (ca[0], ca[1], ca[3]) == (cb[0], cb[1], cb[3]) and cb[2] == -1 and ca[2] > 0, (ca, cb)
     assert L.spt_scene_render_async(sc.handle, C.byref(cam), fr[0].col.data_ptr(), seeds0.data_ptr(),
-                                    fr[0].seeds.data_ptr(), fr[0].px.data_ptr(), w, h, 0, h, 0, 1, 0x200, None,
-                                    st) == rt._lib.RT_ERR_INVALID
+                                    fr[0].seeds.data_ptr(), fr[0].px.data_ptr(), w, h, 0, h, 0, 1, 0x400, None,
+                                    st) == rt._lib.RT_ERR_INVALID      # (0x200 is SPT_COST_MAX)
