@@ -46,7 +46,7 @@ FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: peak FP32 vector
 W, H, SPP = 1920, 1080, 64
 
 
-BENCH_KERNEL = "rt::smallpt::render_kernel<false, false, 0, true, false>"   # the two-query (DUAL) kernel: Cornell has one light
+BENCH_KERNEL = "rt::smallpt::render_kernel<false, false, 0, true, false, 0>"   # the two-query (DUAL) kernel: Cornell has one light
 
 
 def pmc_digest(kernel):
@@ -58,8 +58,12 @@ def pmc_digest(kernel):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if kernel in d:
-            return d[kernel], os.path.relpath(f, ROOT)
+        # (kernel names with and without render_kernel's trailing CG = 0
+        # argument, added in round 5, name the same kernel)
+        norm = {k.replace(", 0>", ">"): k for k in d}
+        key = kernel.replace(", 0>", ">")
+        if key in norm:
+            return d[norm[key]], os.path.relpath(f, ROOT)
     return None, None
 
 

@@ -1687,7 +1687,8 @@ constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2, GEO_WIDE = 3;
 #define RT_WIDE_MINWAVES 4  // the 8-wide (LDS) hierarchy kernels: 126 VGPRs unbounded; 5 or 6 waves per SIMD spill
 #endif
 #ifndef RT_SPT_COOP_G
-#define RT_SPT_COOP_G 8     // lanes per pixel of the cooperative walk (heavy tiles of the 8-wide kernels): 8 or 4
+#define RT_SPT_COOP_G 8     // lanes per pixel of the cooperative walk in windows of <= 5 waves per SIMD (8 or 4;
+                            // windows of 5..10 use 4, launch())
 #endif
 #ifndef RT_WIDE_SPREAD
 #define RT_WIDE_SPREAD 1    // 8-wide persistent kernels: first tier-1 sub-items assigned wave-major (A/B: 0)
@@ -1730,7 +1731,10 @@ constexpr int GS_BYTES = 6160;      // per tile group: 8 x 96 colour floats, 8 x
 // exit position, so a counted shadow query finds the highest-index
 // occluder).  RAYS (SPT_COUNT_RAYS): Intersect / IntersectP calls and samples
 // only, with the uncounted queries (any occluder ends a shadow query).
-template <bool DL, bool COUNT, int GEO, bool DUAL = false, bool RAYS = false>
+// CG (8-wide kernels): lanes per pixel of the cooperative walk this kernel
+// carries (8 or 4), or 0 -- no cooperative code (windows without a
+// cooperative tier: the full frame, N = 2 shares).
+template <bool DL, bool COUNT, int GEO, bool DUAL = false, bool RAYS = false, int CG = 0>
 __global__ void __launch_bounds__(1024, GEO == 2 ? ((COUNT || RAYS) ? RT_BVH_MINWAVES_COUNT : RT_BVH_MINWAVES)
                                               : GEO == 3 ? ((COUNT || RAYS) ? RT_BVH_MINWAVES_COUNT : RT_WIDE_MINWAVES)
                                               : ((DUAL && !COUNT && !RAYS) ? RT_SPT_DUAL_MINWAVES : RT_SPT_MINWAVES))
@@ -1867,7 +1871,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // the hierarchy cooperatively (wide_walk_coop); hs = 2 with split bit 2
     // (G = 4): 4 sub-items of 16 pixels, four lanes per pixel.  Otherwise a
     // sub-item is 64 >> hs pixels, a lane each.
-    const int cg = (GEO == GEO_WIDE && heavy_ && hs == (RT_SPT_COOP_G == 8 ? 3 : 2) && (split & 4)) ? RT_SPT_COOP_G : 0;
+    const int cg = (GEO == GEO_WIDE && CG != 0 && heavy_ && hs == (CG == 8 ? 3 : 2) && (split & 4)) ? CG : 0;
     const bool coop = cg != 0;
     const int sp_ = heavy_ && !coop ? hs : 0;
     const int item = heavy_ ? f >> hs : f - (n1 << hs) + n1;
@@ -2212,8 +2216,11 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 if (!walking) wide_begin<COUNT>(bvh, ray, shadow, t, walk);
                 // (pooled builds: only the cooperative walk here -- the host
                 // launches them with the pool on)
-                walking = coop ? !wide_walk_coop<COUNT, RT_SPT_COOP_G>(bvh, wL, wstk, ray, shadow, walk, split)
-                        : POOLED ? false : !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
+                if constexpr (CG != 0)
+                    walking = coop ? !wide_walk_coop<COUNT, (CG == 4 ? 4 : 8)>(bvh, wL, wstk, ray, shadow, walk, split)
+                                   : POOLED ? false : !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
+                else
+                    walking = POOLED ? false : !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
 #ifdef RT_SPT_TRACE
                 tr_walk += (unsigned)(__builtin_amdgcn_s_memtime() - tr_w0);
 #endif
@@ -2861,7 +2868,7 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
         if (!(work = work_entry(sc, s))) return rtrt::check_launch("spt work counters") ? RT_ERR_HIP : RT_ERR_INVALID;
     }
     // Heavy tiles (with a learnt order, GEO_WIDE persistent launches), in
-    // dispatch order: n1 cooperative tiles (RT_SPT_COOP_G lanes per pixel,
+    // dispatch order: n1 cooperative tiles (8 or 4 lanes per pixel,
     // wide_walk_coop), fetched first by hw waves of each block, then n2 tiles
     // routed one per SIMD beside lighter waves, then the rest.  A window of
     // many waves of work per SIMD (a full frame: 31.6) is throughput-bound:
@@ -2870,28 +2877,38 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
     // which the cooperative walk shortens ~2x at ~3x their issue cost.
     // configs[4], 64 spp (profiles/r03/c4_coop_*.log): N = 8 windows
     // 18.0-19.8 -> 11.4-15.1 ms, N = 4 18.7 -> 17 ms; see DESIGN.md.
-    int n1 = 0, n2 = 0, sp = 0;
+    int n1 = 0, n2 = 0, sp = 0, kcg = 0;
     if (GEO == rt::smallpt::GEO_WIDE && RT_WIDE_PERSIST && g.order && g.tiers) {
         n2 = std::min(4 * g.nblocks, 4 * g.nslots);
         const double wps = (double)g.work / (4.0 * sc.cus);
-        int hw = 0;
+        int hw = 0, cg = RT_SPT_COOP_G;
         if (wps <= 5.0) {
             n1 = 2 * sc.cus;
             hw = 16;
         } else if (wps <= 10.0) {
-            n1 = 2 * sc.cus;
-            hw = 8;
+            // An N = 4 share holds more ~13 ms chains than 512 tiles at
+            // eight lanes per pixel cover (c4_phase_n4.log): twice the tiles
+            // at four lanes per pixel, fetched by every wave of the block
+            // first (one round: 4 sub-items x 1,024 tiles = 16 waves per CU).
+            // N = 4 shares 16.3-16.6 -> 13.8 ms; at N = 8 four lanes lose
+            // (9.9 -> 13.5 ms), c4_coop_g4_ab.log.
+            n1 = 4 * sc.cus;
+            hw = 16;
+            cg = 4;
         }
+        if (const char *e = getenv("RT_WIDE_COOP_G")) cg = atoi(e) == 4 ? 4 : 8;              // A/B
         if (const char *e = getenv("RT_WIDE_COOP")) n1 = std::max(atoi(e), 0);                  // A/B
         if (const char *e = getenv("RT_WIDE_HEAVY_WAVES")) hw = std::min(std::max(atoi(e), 0), 16);   // A/B
         if (n1 > 0) n2 = 0;   // routed tiles beside cooperative ones: N = 4 17 -> 24 ms (c4_coop_tiers_ab.log)
         if (const char *e = getenv("RT_WIDE_HEAVY")) n2 = std::max(atoi(e), 0);                 // A/B
         n1 = std::min(n1, 4 * g.nslots);
         n2 = std::min(n2, 4 * g.nslots - n1);
-        if (n1 > 0) sp = (RT_SPT_COOP_G == 8 ? 3 : 2) | 4 | (hw << 3);
+        if (n1 > 0) sp = (cg == 8 ? 3 : 2) | 4 | (hw << 3);
+        kcg = n1 > 0 ? cg : 0;
         if (const char *e = getenv("RT_SPT_SPLIT")) {   // A/B: tier 1 split 2^k ways, a lane per pixel (k < 3)
             const int k = std::min(std::max(atoi(e), 0), 3);
-            sp = (k == 3 ? (RT_SPT_COOP_G == 8 ? 3 : 2) | 4 : k) | (hw << 3);
+            sp = (k == 3 ? (cg == 8 ? 3 : 2) | 4 : k) | (hw << 3);
+            kcg = k == 3 && n1 > 0 ? cg : 0;
         }
     }
     const int nheavy = std::min(n1, 0xffff) | (std::min(n2, 0xffff) << 16);
@@ -2902,7 +2919,14 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
         split = (RT_WIDE_PERSIST ? sp : 0) | (std::min(std::max(budget, 1), 255) << 8) |
                 (std::min(std::max(batch, 0), 64) << 16) | (std::min(std::max(stop, 0), 64) << 24);
     }
-    hipLaunchKernelGGL((rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS>), dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
+    // (the kernel carries the cooperative walk only when this launch has a
+    // cooperative tier, and only the group size it uses)
+    auto kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 0>;
+    if constexpr (GEO == rt::smallpt::GEO_WIDE) {
+        if (kcg == 8) kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 8>;
+        else if (kcg == 4) kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 4>;
+    }
+    hipLaunchKernelGGL(kern, dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.nslots, g.gstride, first,
                        ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt, work, split,
                        nheavy, sflags);
