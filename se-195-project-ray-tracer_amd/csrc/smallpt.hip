@@ -671,6 +671,9 @@ __device__ __forceinline__ unsigned wide_visit(const uint4 *__restrict__ N, cons
 #ifndef RT_SPT_COOP_LEAN
 #define RT_SPT_COOP_LEAN 1  // cooperative walk: one trip as straight-line selects (N = 8 shares 10.1-10.4 -> 9.9-10.0 ms; A/B: 0)
 #endif
+#ifndef RT_SPT_COOP_LEAFALL
+#define RT_SPT_COOP_LEAFALL 0   // cooperative leaf pass (G = 8): all leaves' distances before any update (A/B)
+#endif
 #ifndef RT_SPT_COOP_LOCAL
 #define RT_SPT_COOP_LOCAL 1 // lean cooperative trip: nearest-hit bests kept per lane, reduced per leaf section
                             // and per query instead of per leaf (N = 8 / 4 shares -2 to -3 %; A/B: 0)
@@ -1359,42 +1362,91 @@ __device__ __forceinline__ bool leaf_coop(const BvhView &B, const ray3 &r, bool 
                 const int q = b + pos + j * G;
                 g[l][j] = B.geo[f[l] + (q < c[l] ? q : 0)];
             }
-#pragma unroll
-        for (int l = 0; l < NL; l++) {
-            if (b >= c[l]) continue;
-            float d[S];
+        if constexpr (G == 8 && RT_SPT_COOP_LEAFALL) {   // (G = 4: two spheres per lane -- the leaf-by-leaf form, no spills)
+            // every leaf's distances first (independent: the lone heavy wave's
+            // issue overlaps them), one range check for all, then the updates
+            float d[NL][S];
             bool bad = false;
-#pragma unroll
-            for (int j = 0; j < S; j++) {
-                const float opx = g[l][j].x - r.o.x, opy = g[l][j].y - r.o.y, opz = g[l][j].z - r.o.z;
-                const float bb = opx * r.d.x + opy * r.d.y + opz * r.d.z;
-                const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g[l][j].w;
-                bad = bad || (b + pos + j * G < c[l] && fabsf(det) < 0x1p-96f);
-                const float sd = sqrt_nr(det);
-                const float t1 = bb - sd, t2 = bb + sd;
-                d[j] = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
-            }
-            if (wave_any(bad)) {
-#pragma unroll
-                for (int j = 0; j < S; j++) d[j] = sphere_hit(g[l][j], r);
-            }
-#pragma unroll
-            for (int j = 0; j < S; j++)
-                if (b + pos + j * G >= c[l]) d[j] = MISS;
-            if (LOCAL && !shadow) {
-#pragma unroll
+    #pragma unroll
+            for (int l = 0; l < NL; l++)
+    #pragma unroll
                 for (int j = 0; j < S; j++) {
-                    const int q = f[l] + b + pos + j * G;
-                    if (d[j] < t) {
-                        t = d[j];
-                        bpos = q;
-                    } else if (d[j] == t) {             // (d finite: a tie)
-                        const int cur_id = bpos >= 0 ? B.id[bpos] : id;
-                        if (B.id[q] > cur_id) bpos = q;
-                    }
+                    const float opx = g[l][j].x - r.o.x, opy = g[l][j].y - r.o.y, opz = g[l][j].z - r.o.z;
+                    const float bb = opx * r.d.x + opy * r.d.y + opz * r.d.z;
+                    const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g[l][j].w;
+                    bad = bad || (b + pos + j * G < c[l] && fabsf(det) < 0x1p-96f);
+                    const float sd = sqrt_nr(det);
+                    const float t1 = bb - sd, t2 = bb + sd;
+                    d[l][j] = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
                 }
-            } else if (leaf_apply<COUNT, G>(B, shadow, maxt, f[l], b, pos, gbase, d, t, bpos, id)) {
-                return true;
+            if (wave_any(bad)) {
+    #pragma unroll
+                for (int l = 0; l < NL; l++)
+    #pragma unroll
+                    for (int j = 0; j < S; j++) d[l][j] = sphere_hit(g[l][j], r);
+            }
+    #pragma unroll
+            for (int l = 0; l < NL; l++)
+    #pragma unroll
+                for (int j = 0; j < S; j++)
+                    if (b + pos + j * G >= c[l]) d[l][j] = MISS;
+    #pragma unroll
+            for (int l = 0; l < NL; l++) {
+                if (b >= c[l]) continue;
+                if (LOCAL && !shadow) {
+    #pragma unroll
+                    for (int j = 0; j < S; j++) {
+                        const int q = f[l] + b + pos + j * G;
+                        if (d[l][j] < t) {
+                            t = d[l][j];
+                            bpos = q;
+                        } else if (d[l][j] == t) {          // (d finite: a tie)
+                            const int cur_id = bpos >= 0 ? B.id[bpos] : id;
+                            if (B.id[q] > cur_id) bpos = q;
+                        }
+                    }
+                } else if (leaf_apply<COUNT, G>(B, shadow, maxt, f[l], b, pos, gbase, d[l], t, bpos, id)) {
+                    return true;
+                }
+            }
+        } else {
+    #pragma unroll
+            for (int l = 0; l < NL; l++) {
+                if (b >= c[l]) continue;
+                float d[S];
+                bool bad = false;
+    #pragma unroll
+                for (int j = 0; j < S; j++) {
+                    const float opx = g[l][j].x - r.o.x, opy = g[l][j].y - r.o.y, opz = g[l][j].z - r.o.z;
+                    const float bb = opx * r.d.x + opy * r.d.y + opz * r.d.z;
+                    const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g[l][j].w;
+                    bad = bad || (b + pos + j * G < c[l] && fabsf(det) < 0x1p-96f);
+                    const float sd = sqrt_nr(det);
+                    const float t1 = bb - sd, t2 = bb + sd;
+                    d[j] = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
+                }
+                if (wave_any(bad)) {
+    #pragma unroll
+                    for (int j = 0; j < S; j++) d[j] = sphere_hit(g[l][j], r);
+                }
+    #pragma unroll
+                for (int j = 0; j < S; j++)
+                    if (b + pos + j * G >= c[l]) d[j] = MISS;
+                if (LOCAL && !shadow) {
+    #pragma unroll
+                    for (int j = 0; j < S; j++) {
+                        const int q = f[l] + b + pos + j * G;
+                        if (d[j] < t) {
+                            t = d[j];
+                            bpos = q;
+                        } else if (d[j] == t) {             // (d finite: a tie)
+                            const int cur_id = bpos >= 0 ? B.id[bpos] : id;
+                            if (B.id[q] > cur_id) bpos = q;
+                        }
+                    }
+                } else if (leaf_apply<COUNT, G>(B, shadow, maxt, f[l], b, pos, gbase, d, t, bpos, id)) {
+                    return true;
+                }
             }
         }
     }
