@@ -544,7 +544,7 @@ def list_tiled_line(dev, rank, world, distributed, s, sc, cm, spp, workload, fra
             s.wait_event(freed[b])
         if i is not None:
             rev[i][0].record(s)
-        render(mine, b)
+        render(mine, b, flags=rtamd.SPT_LIST_SET)          # (balanced_partition's lists are sets)
         if i is not None:
             rev[i][1].record(s)
         if world > 1:

@@ -148,6 +148,13 @@ int rtw_render_ocl_async(const rt_primitive *d_prims, int nprims, uint32_t *d_xr
  * pixel chain, the order key for the heavy-tile treatment (list such groups
  * first), where the sum is the load to balance. */
 #define SPT_COST_MAX 0x200
+/* Flag OR-ed into `mode` of spt_scene_render_list_async only: the caller
+ * guarantees that d_groups is already a set (no repeats, every entry in
+ * range -- rtamd.dist.ListGather checks its lists on the host), so the
+ * per-call dedup pass (a stream-ordered scratch allocation, a fill, one
+ * small kernel, the free) is skipped.  A list that breaks the promise may
+ * render a group twice in one launch: results are then undefined. */
+#define SPT_LIST_SET 0x800
 
 /* Blocking, host buffers, whole frame.  Runs samples first_sample ..
  * first_sample+nsamples-1 of every pixel, exactly as nsamples successive
@@ -230,7 +237,11 @@ int spt_group_count(int w, int h);
  * balanced on measured costs (rtamd.dist.balanced_partition).  d_group_cost
  * (nullable, device, spt_group_count(w, h) words; hierarchy scenes only,
  * left unchanged otherwise): each listed group's wave time in 100 MHz ticks
- * is ADDED to its entry (zero it first).  No order is learnt on this path.
+ * is ADDED to its entry (zero it first).  With full counters (d_counters
+ * set, no SPT_COUNT_RAYS) a lane that finishes its pixel takes the next one
+ * (pixel refill), so there the unit is a pixel: the entry receives the sum
+ * of its pixels' durations, or with SPT_COST_MAX the longest one -- a lane
+ * time, not a wave time.  No order is learnt on this path.
  * Same results per pixel as any other window. */
 int spt_scene_render_list_async(const spt_scene *scene, const rt_camera *camera, float *d_colors,
                                 const uint32_t *d_seeds_in, uint32_t *d_seeds_out, uint32_t *d_pixels,

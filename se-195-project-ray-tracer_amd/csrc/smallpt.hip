@@ -2073,8 +2073,11 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                         }
                         seeds_out[2 * (size_t)i] = s0;
                         seeds_out[2 * (size_t)i + 1] = s1;
-                        if (SCHED && group_cost)        // the pixel's duration, summed per group
-                            atomicAdd(&group_cost[pgrp], (unsigned)__builtin_amdgcn_s_memrealtime() - pix_t0);
+                        if (SCHED && group_cost) {      // the pixel's duration: per group the sum, or
+                            const unsigned dur = (unsigned)__builtin_amdgcn_s_memrealtime() - pix_t0;
+                            if (sflags & 4) atomicMax(&group_cost[pgrp], dur);   //   (cost_max) the longest
+                            else atomicAdd(&group_cost[pgrp], dur);
+                        }
                     }
                     const unsigned long long need = __builtin_amdgcn_ballot_w64(want);
                     const int ncl = __builtin_popcountll(need);
@@ -3147,7 +3150,15 @@ extern "C" int spt_scene_create(const rt_sphere *spheres, unsigned nspheres, spt
         if (!((q.e.x == 0.f) && (q.e.x == 0.f) && (q.e.z == 0.f))) lights.push_back(i);  // vec.h:44
     }
     sc->nlights = (int)lights.size();
-    sc->no_refr = std::none_of(spheres, spheres + nspheres, [](const rt_sphere &q) { return q.refl == 2; });   // REFR
+    // render_kernel's branch order (geomfunc.h:223-281): an emitter (the
+    // viszero test of vec.h:44, x tested twice) ends the path, then refl ==
+    // DIFF, refl == SPEC, and EVERY other refl value takes the REFR branch
+    // (:281 `else`) -- refl 2, but also 3 or -1.  Only a scene whose every
+    // non-emitter is DIFF or SPEC may skip the refraction terms.
+    sc->no_refr = std::all_of(spheres, spheres + nspheres, [](const rt_sphere &q) {
+        const bool emitter = !((q.e.x == 0.f) && (q.e.x == 0.f) && (q.e.z == 0.f));
+        return emitter || q.refl == 0 || q.refl == 1;
+    });
     if (lights.empty())                    // one zero record (render_kernel loads light 0 unconditionally)
         soa.insert(soa.end(), 3, make_float4(0.f, 0.f, 0.f, 0.f));
     for (int i : lights) {                 // light records: geo, col, emi of each light, ascending
@@ -3412,9 +3423,14 @@ extern "C" int spt_scene_render_list_async(const spt_scene *sc, const rt_camera 
     if (total < 0) return total;
     if (ngroups < 0 || ngroups > total || (ngroups > 0 && !d_groups))
         return rtrt::fail(RT_ERR_INVALID, "spt_scene_render_list_async: need 0 <= ngroups <= spt_group_count(w, h)");
+    const bool is_set = (mode & SPT_LIST_SET) != 0;
+    mode &= ~SPT_LIST_SET;
     int rc = check_render_args(camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, 0, h, first_sample,
                                nsamples, mode);
     if (rc || ngroups == 0) return rc;
+    if (is_set)                           // (the caller's promise: no dedup pass)
+        return scene_render(sc, camera, d_colors, d_seeds_in, d_seeds_out, d_pixels, w, h, 0, h, 1, first_sample,
+                            nsamples, mode, d_counters, stream, d_groups, ngroups, d_group_cost);
     // The list as a set (list_dedup_kernel): repeated entries render once.
     // Stream-ordered scratch (graph-capturable): ngroups entries + the claim bits.
     hipStream_t s = (hipStream_t)stream;

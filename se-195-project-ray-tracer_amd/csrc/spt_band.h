@@ -34,6 +34,17 @@ inline size_t send_offset(int w, int h, int n, int k) { return (size_t)k * gathe
 // Colour floats of the padded buffer (N * B rows).
 inline size_t padded_floats(int w, int h, int n) { return (size_t)n * gather_count(w, h, n); }
 
+// The pixel-row windows a band's device repacks after the gather -- every
+// row it did not render: win[0] = [win[0][0], win[0][1]) below its own pixel
+// rows [h - s1, h - s0), win[1] above them (either may be empty).
+inline void repack_windows(int h, int s0, int s1, int win[2][2])
+{
+    win[0][0] = 0;
+    win[0][1] = h - s1;
+    win[1][0] = h - s0;
+    win[1][1] = h;
+}
+
 }  // namespace sptband
 
 #endif

@@ -340,9 +340,11 @@ extern "C" int spt_multi_gather_async(spt_multi *m)
     // hold the render call's pack of the same colours).
     for (Band &b : m->bands) {
         if ((rc = scope.select(b.device))) return rc;
-        const int r0 = m->h - b.s1, r1 = m->h - b.s0;
-        if (r0 > 0 && (rc = spt_pack_pixels_async(b.d_col, b.d_px, m->w, m->h, 0, r0, b.stream))) return rc;
-        if (r1 < m->h && (rc = spt_pack_pixels_async(b.d_col, b.d_px, m->w, m->h, r1, m->h, b.stream))) return rc;
+        int win[2][2];
+        sptband::repack_windows(m->h, b.s0, b.s1, win);
+        for (const auto &wn : win)
+            if (wn[1] > wn[0] && (rc = spt_pack_pixels_async(b.d_col, b.d_px, m->w, m->h, wn[0], wn[1], b.stream)))
+                return rc;
     }
     return RT_OK;
 }

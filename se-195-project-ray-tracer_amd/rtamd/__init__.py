@@ -19,12 +19,12 @@ import numpy as np
 
 from . import ppm, scenes
 from ._lib import (Camera, Float4, Primitive, QPrimitive, RTError, Sphere, Vec3, check, device_count, lib,
-                   set_device, SPT_COST_MAX, SPT_COUNT_RAYS, SPT_DIRECT_LIGHTING, SPT_PATH_TRACING)
+                   set_device, SPT_COST_MAX, SPT_COUNT_RAYS, SPT_LIST_SET, SPT_DIRECT_LIGHTING, SPT_PATH_TRACING)
 
 __all__ = ["Camera", "Primitive", "QPrimitive", "Float4", "Sphere", "Vec3", "RTError", "scenes", "lib", "check",
            "device_count", "set_device", "whitted_render", "queue_render", "SmallptFrame", "SmallptScene",
            "SmallptMulti",
-           "SPT_PATH_TRACING", "SPT_DIRECT_LIGHTING", "SPT_COUNT_RAYS", "SPT_COST_MAX"]
+           "SPT_PATH_TRACING", "SPT_DIRECT_LIGHTING", "SPT_COUNT_RAYS", "SPT_COST_MAX", "SPT_LIST_SET"]
 
 
 def whitted_render(w, h, row_begin=20, row_end=None, prims=None, nprims=None, frame=None,

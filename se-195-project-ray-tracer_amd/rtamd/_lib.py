@@ -15,6 +15,7 @@ RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NODEVICE = 0, -1, -2, -3
 SPT_PATH_TRACING, SPT_DIRECT_LIGHTING = 0, 1
 SPT_COUNT_RAYS = 0x100
 SPT_COST_MAX = 0x200
+SPT_LIST_SET = 0x800
 
 # Every symbol include/rt_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = ("rt_last_error", "rt_device_count", "rt_set_device", "rt_release", "rt_cached_bytes",

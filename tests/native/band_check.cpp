@@ -5,8 +5,10 @@
 //    (send_offset) is exactly where its real rows sit in the full buffer;
 //  * every chunk lies inside the padded buffer, and only rows >= h of it are
 //    padding (a chunk holds padding only past its band's real rows);
-//  * the repack windows each device runs after the gather ([0, h - s1) and
-//    [h - s0, h) in pixel rows) cover exactly the rows it did not render.
+//  * the repack windows each device runs after the gather (repack_windows,
+//    the helper spt_multi.hip calls) and the pixel rows its band renders
+//    (the flip of its slot rows, derived independently) cover every pixel
+//    row exactly once.
 // Prints the number of (h, N) cases checked, or the first failure.
 #include <stdio.h>
 #include <vector>
@@ -35,13 +37,20 @@ int main()
                     const bool real = r >= s0 && r < s1;
                     if (real != (r < h)) { printf("FAIL chunk h=%d n=%d k=%d r=%d\n", h, n, k, r); return 1; }
                 }
-                // repack: pixel rows [0, h - s1) and [h - s0, h) = all but the band's own
+                // repack (the windows spt_multi.hip takes from repack_windows)
+                // plus the pixel rows the band renders itself -- smallptCPU.cpp:86's
+                // flip of its slot rows [s0, s1), derived here pixel by pixel --
+                // cover every pixel row exactly once
                 std::vector<int> seen(h, 0);
-                for (int y = 0; y < h - s1; y++) seen[y]++;
-                for (int y = h - s0; y < h; y++) seen[y]++;
-                for (int y = h - s1; y < h - s0; y++) seen[y] += 2;
+                int win[2][2];
+                sptband::repack_windows(h, s0, s1, win);
+                for (const auto &wn : win) {
+                    if (wn[0] < 0 || wn[1] > h) { printf("FAIL window h=%d n=%d k=%d\n", h, n, k); return 1; }
+                    for (int y = wn[0]; y < wn[1]; y++) seen[y]++;
+                }
+                for (int slot_row = s0; slot_row < s1; slot_row++) seen[h - 1 - slot_row]++;
                 for (int y = 0; y < h; y++)
-                    if (seen[y] != (y >= h - s1 && y < h - s0 ? 2 : 1)) { printf("FAIL repack h=%d n=%d k=%d\n", h, n, k); return 1; }
+                    if (seen[y] != 1) { printf("FAIL repack h=%d n=%d k=%d y=%d\n", h, n, k, y); return 1; }
             }
             if (next != h) { printf("FAIL cover h=%d n=%d\n", h, n); return 1; }
             cases++;

@@ -1,7 +1,10 @@
-"""Multi-rank sharding (rtamd.dist) on CPU with gloo, world size 2 and 4:
-each rank renders its row band with the CPU oracle, the bands are
-all-gathered, and the assembled frame must equal a single-rank render
-bit for bit (tiles are disjoint, so sharding is exact)."""
+"""Multi-rank sharding (rtamd.dist) on CPU with gloo, world sizes 2 to 8
+(the 8-GPU node's rank count): each rank renders its share -- a row band,
+its interleaved 8-row groups, or a cost-balanced tile-group list -- with the
+CPU oracle, the shares are all-gathered, and the assembled frame must equal
+a single-rank render bit for bit (tiles are disjoint, so sharding is exact).
+Ragged frames (h not a multiple of 8 x world) leave ranks with short or
+empty shares."""
 import os
 import socket
 import subprocess
@@ -21,7 +24,7 @@ import oracle_lib as O
 from rtamd import dist as rd
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 dist.init_process_group("gloo")
-w, h, spp = 48, 32, 3
+w, h, spp = %(w)d, %(h)d, 3
 S, n = O.cornell(); cam = O.cornell_camera(w, h)
 col = np.zeros(3 * w * h, np.float32); seeds = O.seeds(w, h); px = np.zeros(w * h, np.uint32)
 tc, tp, ts = torch.from_numpy(col), torch.from_numpy(px.view(np.int32)), torch.from_numpy(seeds.view(np.int32))
@@ -79,12 +82,16 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("world,mode", [(2, "bands"), (4, "bands"), (2, "groups"), (3, "groups"), (2, "lists"),
-                                        (3, "lists")])
-def test_band_gather_is_exact(tmp_path, world, mode):
+@pytest.mark.parametrize("world,mode,w,h", [
+    (2, "bands", 48, 32), (4, "bands", 48, 32), (8, "bands", 48, 32),
+    (2, "groups", 48, 32), (3, "groups", 48, 32),
+    (8, "groups", 48, 32),      # 4 groups: ranks 4..7 render nothing and still join the gather
+    (8, "groups", 40, 70),      # ragged: 9 groups, the last 6 rows (h not a multiple of 8 x 8)
+    (2, "lists", 48, 32), (3, "lists", 48, 32), (8, "lists", 48, 32), (8, "lists", 40, 70)])
+def test_band_gather_is_exact(tmp_path, world, mode, w, h):
     script = tmp_path / "w.py"
     script.write_text(WORKER % {"pkg": os.path.join(ROOT, "se-195-project-ray-tracer_amd"),
-                                "tests": HERE, "mode": mode})
+                                "tests": HERE, "mode": mode, "w": w, "h": h})
     port = _port()
     procs = []
     for r in range(world):

@@ -67,11 +67,12 @@ def test_lists_partition_the_frame(rt, monkeypatch, kind, w, h, spp, env):
     perm = rng.permutation(ng)
     cuts = sorted(rng.choice(np.arange(1, ng), 2, replace=False))
     lists = [perm[:cuts[0]], perm[cuts[0]:cuts[1]], perm[cuts[1]:]]
-    for mode in (0, rt.SPT_COUNT_RAYS):
+    for mode in (0, rt.SPT_COUNT_RAYS, rt.SPT_LIST_SET):
         got = _Frame(torch, dev, w, h, seeds0)
         got.cnt[2] = 12345                                 # rays-only leaves counters[2] untouched
         for i, lst in enumerate(lists):
-            lst = list(lst) + ([-7, ng, 1 << 30] if i == 1 else [])   # out-of-range entries: skipped
+            # out-of-range entries: skipped (SPT_LIST_SET: the caller promises none, and no dedup pass runs)
+            lst = list(lst) + ([-7, ng, 1 << 30] if i == 1 and mode != rt.SPT_LIST_SET else [])
             d = torch.tensor(lst, dtype=torch.int32, device=dev)
             rt.check(L.spt_scene_render_list_async(sc.handle, C.byref(cam), got.col.data_ptr(), seeds0.data_ptr(),
                                                    got.seeds.data_ptr(), got.px.data_ptr(), w, h, d.data_ptr(),
@@ -79,7 +80,7 @@ def test_lists_partition_the_frame(rt, monkeypatch, kind, w, h, spp, env):
         torch.cuda.synchronize()
         assert got.same(ref, torch), mode
         c, r = got.cnt.tolist(), ref.cnt.tolist()
-        if mode:
+        if mode == rt.SPT_COUNT_RAYS:
             assert (c[0], c[1], c[3]) == (r[0], r[1], r[3]) and c[2] == 12345, (c, r)
         else:
             assert c == [r[0], r[1], r[2] + 12345, r[3]], (c, r)
@@ -126,6 +127,28 @@ def test_list_costs_and_bad_arguments(rt):
     ratio = m[mask].sum() / c[mask].sum()
     assert 0.15 < ratio < 0.9, ratio
     assert torch.equal(f2.col.view(torch.int32), f.col.view(torch.int32)) and torch.equal(f2.px, f.px)
+    # Full counters (the refilling kernel: a lane's unit is a pixel): the sum
+    # of each group's pixel durations, or with SPT_COST_MAX the longest one --
+    # which no launch can exceed (100 MHz ticks against the launch's own
+    # duration), while a sum over a group's pixels far exceeds its max.
+    csum = torch.zeros(ng, dtype=torch.int32, device=dev)
+    cmx = torch.zeros(ng, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+    for mode, cb in ((0, csum), (rt.SPT_COST_MAX, cmx)):
+        f3 = _Frame(torch, dev, w, h, seeds0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rt.check(L.spt_scene_render_list_async(sc.handle, C.byref(cam), f3.col.data_ptr(), seeds0.data_ptr(),
+                                               f3.seeds.data_ptr(), f3.px.data_ptr(), w, h, d.data_ptr(), len(lst), 0,
+                                               2, mode, cnt.data_ptr(), cb.data_ptr(), st))
+        e1.record()
+        torch.cuda.synchronize()
+        assert torch.equal(f3.col.view(torch.int32), f.col.view(torch.int32)) and torch.equal(f3.px, f.px)
+    launch_ticks = e0.elapsed_time(e1) * 1e5
+    s, mx = csum.cpu().numpy().astype(np.int64), cmx.cpu().numpy().astype(np.int64)
+    assert (mx[mask] > 0).all() and (mx[~mask] == 0).all() and (s[mask] > 0).all()
+    assert mx.max() <= 1.05 * launch_ticks + 1000, (mx.max(), launch_ticks)
+    assert mx[mask].sum() < 0.5 * s[mask].sum(), (mx[mask].sum(), s[mask].sum())
     assert L.spt_scene_render_list_async(sc.handle, C.byref(cam), f2.col.data_ptr(), seeds0.data_ptr(),
                                          f2.seeds.data_ptr(), f2.px.data_ptr(), w, h, d.data_ptr(), len(lst), 0, 1,
                                          0x400, None, None, st) == rt._lib.RT_ERR_INVALID

@@ -111,6 +111,23 @@ def test_large_scene_hierarchy_vs_oracle(rt, oracle):
     _check((f.colors, f.seeds, f.pixels, f.counters), ref)
 
 
+@pytest.mark.parametrize("nonstd", [3, -1])
+def test_nonstandard_refl_takes_refr_branch(rt, oracle, nonstd):
+    """geomfunc.h:281: every refl that is neither DIFF (0) nor SPEC (1) takes
+    the REFR branch.  A hierarchy scene (configs[4]'s spheres, all DIFF, so
+    normally run with the light-only pass A) with some spheres set to a
+    non-standard refl must still refract there, as the oracle does."""
+    spheres, n, cam = rt.scenes.complex10k()
+    for i in range(2, n, 5):                 # (0: the light, 1: the ground)
+        spheres[i].refl = nonstd
+    w, h = 48, 32
+    rt.scenes.update_camera(cam, w, h)
+    f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n, camera=cam)
+    f.render(2)
+    ref = _oracle_frame(oracle, w, h, [2], spheres=(spheres, n), cam=cam)
+    _check((f.colors, f.seeds, f.pixels, f.counters), ref)
+
+
 @pytest.mark.parametrize("env", [{"RT_SPT_NO_BVH": "1"}, {"RT_SPT_GEO": "global"}])
 def test_large_scene_global_path(rt, oracle, env, monkeypatch):
     """The global-SoA full-scan kernel (GEO_GLOBAL: scenes above the LDS
