@@ -80,8 +80,8 @@ int join_aux_on_error(DeviceState &st, hipStream_t s, int rc);
 void release_cached_scenes();
 // Frees spt_render_multi's cached band context (spt_multi.hip; rt_release).
 void release_cached_multi();
-// The environment knobs spt_scene_create reads (RT_SPT_NO_BVH, RT_SPT_GEO,
-// RT_SPT_WIDE, RT_SPT_WIDE_LEAF, RT_WIDE_WPB) as one key: the scene caches
+// The environment test hooks spt_scene_create reads (RT_SPT_NO_BVH,
+// RT_SPT_GEO, RT_SPT_WIDE) as one key: the scene caches
 // of spt_render and spt_render_multi rebuild when it changes (smallpt.hip).
 std::string scene_prep_hooks();
 // The calling thread's rt_set_device choice (-1: none, HIP's current device).

@@ -272,14 +272,11 @@ struct BvhView {
                           //   staged by the counted kernels only)
     int wnodes, wdepth;   //   its node count and depth (levels of wide nodes)
 };
-constexpr float BVH_ALPHA_R = 1.f / 64.f;   // per node, with BETA, in the node record
+// (BVH_ALPHA_R = spt_bvh.h's ALPHA_R: applied on the host, in the node records' margin terms)
 #ifndef RT_BVH_K
 #define RT_BVH_K 2.f
 #endif
 
-#ifndef RT_BVH_LEAF_BF
-#define RT_BVH_LEAF_BF 1    // branch-free leaf sphere tests (configs[4] 40.5 -> 39.5 ms; 0 = per-sphere branch, A/B)
-#endif
 #ifndef RT_BVH_BUDGET
 #define RT_BVH_BUDGET 32    // walk steps per render-loop iteration before a lane's query is suspended
 #endif
@@ -299,18 +296,6 @@ constexpr int BVH_LEAF_MAX = 4;             // spheres per leaf (host build: BVH
 // indices before the first test, so a step costs one memory latency (a first
 // form that branched on the link word first and loaded per sphere paid two
 // to five: configs[4] 11.1 -> 8.5 ms per 4 spp).
-// Tools-only traversal statistics (build with -DRT_BVH_STATS; read by
-// spt_bvh_stats_read): lane node visits, lane crossed leaves, lane sphere
-// tests, wave loop trips, wave leaf-block executions, lane queries, wave
-// queries.  Never in the product build.
-#ifdef RT_BVH_STATS
-__device__ unsigned long long g_bvh_stats[24];
-#define BVH_ST(k, v) st[k] += (v)
-#define BVH_ST_WAVE(k) do { if ((int)(threadIdx.x & 63) == __builtin_ctzll(__builtin_amdgcn_read_exec())) st[k]++; } while (0)
-#else
-#define BVH_ST(k, v) do {} while (0)
-#define BVH_ST_WAVE(k) do {} while (0)
-#endif
 
 // A query's walk state, kept across loop iterations of render_kernel: the
 // walk is resumable, so a lane whose walk is long does not hold up the
@@ -318,25 +303,17 @@ __device__ unsigned long long g_bvh_stats[24];
 // continues).  t = nearest distance so far (any hit: maxt, unchanged), id =
 // the result so far, node = next node in the ray's octant layout (nnodes:
 // finished), pend = a crossed leaf not yet tested (first | count << 24).
-#ifndef RT_BVH_PEND2
-#define RT_BVH_PEND2 1      // a lane may hold two crossed leaves and keeps stepping while it holds one
-#endif
-#ifndef RT_BVH_BATCH        // leaf postponement: test pending leaves once >= BATCH/64 of the lanes in the walk
-#if RT_BVH_PEND2            //   cannot step (hold two leaves, or reached the end with one) -- else: hold one
-#define RT_BVH_BATCH 16
-#else
-#define RT_BVH_BATCH 32
-#endif
-#endif
+// Leaf postponement: a lane may hold two crossed leaves and keeps stepping
+// while it holds one; the wave tests pending leaves once >= BVH_BATCH/64 of
+// its lanes in the walk cannot step (hold two, or reached the end with one).
+constexpr int BVH_BATCH = 16;
 struct BvhWalk {
     float t;
     int id, node, pend;
     unsigned m;             // 8-wide walk: node = the current node (-1: root not yet visited), m = its
     int sp, bpos;           //   children still to visit (visit order), sp = stacked (node, mask) entries,
                             //   bpos = hierarchy position of the best leaf hit so far (-1: none)
-#if RT_BVH_PEND2
     int pend2;              // a second crossed leaf (only while pend holds one)
-#endif
 #ifdef RT_SPT_TRACE
     unsigned tr_leaf, tr_trips, tr_leafruns;   // tools-only phase stamps (s_memtime cycles, counts)
 #endif
@@ -375,9 +352,7 @@ __device__ __forceinline__ void bvh_begin(const BvhView &B, const ray3 &r, bool 
     W.id = id;
     W.node = (!COUNT && shadow && id >= 0) ? B.nnodes : 0;
     W.pend = 0;
-#if RT_BVH_PEND2
     W.pend2 = 0;
-#endif
 }
 
 // Advances the walks of the wave's lanes by up to RT_BVH_BUDGET steps
@@ -389,19 +364,9 @@ __device__ __forceinline__ void bvh_begin(const BvhView &B, const ray3 &r, bool 
 template <bool COUNT>
 __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &W)
 {
-#ifdef RT_BVH_STATS
-    unsigned st[24] = {};
-    BVH_ST(5, W.node == 0 && W.pend == 0);
-    BVH_ST_WAVE(6);
-#endif
     const float maxt = W.t;
     float t = W.t;
-    int id = W.id, node = W.node, pend = W.pend;
-#if RT_BVH_PEND2
-    int pend2 = W.pend2;
-#else
-    constexpr int pend2 = 0;
-#endif
+    int id = W.id, node = W.node, pend = W.pend, pend2 = W.pend2;
     // Slab test (culling only: its rounding is inside the margin; fused ops
     // are fine here and nowhere else).  Zero direction components become
     // +-1e-30 so no 0 * inf appears.
@@ -415,9 +380,9 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
     // element offset from the uniform base (one VGPR, not a 64-bit pointer).
     const unsigned lay = 2u * (unsigned)B.nnodes * ((dx < 0.f ? 1u : 0u) | (dy < 0.f ? 2u : 0u) | (dz < 0.f ? 4u : 0u));
     // Crossed leaves are postponed: a lane that reaches one keeps it pending
-    // and steps on until it holds a second (RT_BVH_PEND2; else it stops at
-    // the first); the wave tests one pending leaf per lane together once at
-    // least RT_BVH_BATCH/64 of its lanes still in the walk cannot step (or
+    // and steps on until it holds a second; the wave tests one pending leaf
+    // per lane together once at least BVH_BATCH/64 of its lanes still in the
+    // walk cannot step (or
     // none can), instead of running the leaf block for the one or two lanes
     // that reach a leaf in a given step.  The result does not depend on the
     // order spheres are tested in (minimum, ties to the highest index; or
@@ -425,12 +390,7 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
     // the culling limit t of the steps in between looser, never wrong.
     int trips = 0;
     while (true) {
-        if (node < B.nnodes && (RT_BVH_PEND2 ? pend2 == 0 : pend == 0)) {
-            BVH_ST(0, 1);
-            BVH_ST(21, node < 64);
-            BVH_ST(22, node < 256);
-            BVH_ST(23, node < 1024);
-            BVH_ST_WAVE(3);
+        if (node < B.nnodes && pend2 == 0) {
             const float4 a = B.node[lay + 2u * (unsigned)node], b = B.node[lay + 2u * (unsigned)node + 1u];
             const int link = __float_as_int(a.w);
             const float lim = shadow ? maxt : t;
@@ -445,48 +405,33 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
             int next = cross ? node + 1 : link;
             if (link < 0) {                              // leaf ~(first | count << 24); escape = next node
                 next = node + 1;
-#if RT_BVH_PEND2
                 if (cross) {
                     if (pend == 0) pend = ~link;
                     else pend2 = ~link;
                 }
-#else
-                if (cross) pend = ~link;
-#endif
             }
             node = next;
         }
         trips++;
         const unsigned long long pm = __builtin_amdgcn_ballot_w64(pend != 0);
-        const unsigned long long sm = __builtin_amdgcn_ballot_w64(node < B.nnodes && (RT_BVH_PEND2 ? pend2 == 0 : pend == 0));
+        const unsigned long long sm = __builtin_amdgcn_ballot_w64(node < B.nnodes && pend2 == 0);
         if (pm == 0) {
             if (sm == 0 || trips >= RT_BVH_BUDGET) break;
             continue;
         }
-#if RT_BVH_PEND2
-        // leaves tested once half the lanes in the walk cannot step
         if (sm != 0 && trips < RT_BVH_BUDGET &&
-            64 * __builtin_popcountll(pm & ~sm) < RT_BVH_BATCH * __builtin_popcountll(pm | sm))
+            64 * __builtin_popcountll(pm & ~sm) < BVH_BATCH * __builtin_popcountll(pm | sm))
             continue;
-#else
-        if (sm != 0 && trips < RT_BVH_BUDGET &&
-            64 * __builtin_popcountll(pm) < RT_BVH_BATCH * __builtin_popcountll(pm | sm))
-            continue;
-#endif
 #ifdef RT_SPT_TRACE
         const unsigned long long tr_l0 = __builtin_amdgcn_s_memtime();
         W.tr_leafruns++;
 #endif
         if (pend != 0) {
             const int f = pend & 0xffffff, c = pend >> 24;
-            BVH_ST(1, 1);
-            BVH_ST(2, c);
-            BVH_ST_WAVE(4);
             float4 g[BVH_LEAF_MAX];
 #pragma unroll
             for (int q = 0; q < BVH_LEAF_MAX; q++)        // all loads first: one latency per leaf
                 g[q] = B.geo[f + (q < c ? q : 0)];
-#if RT_BVH_LEAF_BF
             // Branch-free sphere tests (as query_bf): sqrt_nr is exact for det
             // in [2^-96, inf) and NaN below 0 (a miss); a wave with a lane
             // meeting 0 <= |det| < 2^-96 redoes the leaf with sphere_hit.
@@ -535,32 +480,12 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
                 }
             }
             if (bpos >= 0) id = B.id[bpos];
-#else
-#pragma unroll
-            for (int q = 0; q < BVH_LEAF_MAX; q++) {
-                if (q < c) {
-                    const float d = sphere_hit(g[q], r);
-                    const int i = B.id[f + q];
-                    if (shadow) {
-                        if (d < maxt && i > id) id = i;
-                    } else if (d < t || (d == t && i > id)) {
-                        t = d;
-                        id = i;
-                    }
-                }
-            }
-#endif
-#if RT_BVH_PEND2
             if (!COUNT && shadow && id >= 0) {
                 node = B.nnodes;
                 pend2 = 0;
             }
             pend = pend2;
             pend2 = 0;
-#else
-            if (!COUNT && shadow && id >= 0) node = B.nnodes;
-            pend = 0;
-#endif
         }
 #ifdef RT_SPT_TRACE
         W.tr_leaf += (unsigned)(__builtin_amdgcn_s_memtime() - tr_l0);
@@ -574,26 +499,7 @@ __device__ bool bvh_walk(const BvhView &B, const ray3 &r, bool shadow, BvhWalk &
     W.id = id;
     W.node = node;
     W.pend = pend;
-#if RT_BVH_PEND2
     W.pend2 = pend2;
-#endif
-#ifdef RT_BVH_STATS
-    {
-        const float4 a0 = B.node[lay], b0 = B.node[lay + 1u];
-        const bool far = fabsf(r.o.x - a0.x) > b0.x || fabsf(r.o.y - a0.y) > b0.y || fabsf(r.o.z - a0.z) > b0.z;
-        st[7] = W.node >= B.nnodes && st[0] >= 128; st[8] = st[0] >= 512; st[9] = st[0] >= 2048;
-        st[10] = far ? st[0] : 0; st[11] = far; st[12] = shadow; st[13] = shadow ? st[0] : 0;
-        st[14] = far && st[0] >= 512;
-        st[15] = alpha > 1.f / 128.f; st[16] = st[15] ? st[0] : 0;
-        const float ox = r.o.x - a0.x, oy = r.o.y - a0.y, oz = r.o.z - a0.z;
-        const float R0 = sqrtf(b0.x * b0.x + b0.y * b0.y + b0.z * b0.z);
-        const bool vfar = ox * ox + oy * oy + oz * oz > 64.f * R0 * R0;
-        st[17] = vfar; st[18] = vfar ? st[0] : 0; st[19] = vfar && st[0] >= 512; st[20] = st[15] && st[0] >= 512;
-    }
-#pragma unroll
-    for (int k = 0; k < 24; k++)
-        if (st[k]) atomicAdd(&g_bvh_stats[k], (unsigned long long)st[k]);   // divergent: per-lane atomics
-#endif
     return node >= B.nnodes && pend == 0;
 }
 
@@ -668,25 +574,12 @@ __device__ __forceinline__ unsigned wide_visit(const uint4 *__restrict__ N, cons
     return hm;
 }
 
-#ifndef RT_SPT_COOP_LEAN
-#define RT_SPT_COOP_LEAN 1  // cooperative walk: one trip as straight-line selects (N = 8 shares 10.1-10.4 -> 9.9-10.0 ms; A/B: 0)
-#endif
-#ifndef RT_SPT_COOP_LEAFALL
-#define RT_SPT_COOP_LEAFALL 0   // cooperative leaf pass (G = 8): all leaves' distances before any update (A/B)
-#endif
-#ifndef RT_SPT_COOP_LOCAL
-#define RT_SPT_COOP_LOCAL 1 // lean cooperative trip: nearest-hit bests kept per lane, reduced per leaf section
-                            // and per query instead of per leaf (N = 8 / 4 shares -2 to -3 %; A/B: 0)
-#endif
 #ifndef RT_SPT_COOP_NL
 #define RT_SPT_COOP_NL 2    // cooperative walk: leaves tested per pass (loads in flight together)
 #endif
-#ifndef RT_WIDE_BUDGET
-#define RT_WIDE_BUDGET 16   // wide-walk trips per render-loop iteration before a lane's query is suspended
-#endif
-#ifndef RT_WIDE_STOP
-#define RT_WIDE_STOP 32     // wide walk: end the call once <= STOP/64 of its lanes still walk (configs[4] 36.3 -> 29.0 ms)
-#endif
+// (wide_walk's trip budget per call (16), leaf batch threshold (16/64) and
+// early stop (end the call once <= 32/64 of its lanes still walk: configs[4]
+// 36.3 -> 29.0 ms) come from the host, SptTune.)
 constexpr int WIDE_WORDS = 28;   // per node (spt_bvh.h)
 
 template <bool COUNT>
@@ -699,7 +592,7 @@ __device__ __forceinline__ void wide_begin(const BvhView &B, const ray3 &r, bool
     W.sp = 0;
 }
 
-// Advances the wave's wide walks by up to RT_WIDE_BUDGET trips; returns true
+// Advances the wave's wide walks by up to `budget` trips; returns true
 // for a lane whose query is complete (results as bvh_walk).  L: the block's
 // LDS copy of the nodes; stk: this wave's LDS stack (entry k of lane l at
 // stk[64 k + l]).  Crossed leaves are postponed and tested together as in
@@ -862,289 +755,6 @@ __device__ bool wide_walk(const BvhView &B, const uint4 *__restrict__ L, unsigne
     W.pend = pend;
     W.pend2 = pend2;
     return done;
-}
-
-// ---------------------------------------------------------------------------
-// Block pool of pending walks (RT_WIDE_POOL, uncounted 8-wide kernels).
-// wide_walk leaves a lane idle from the trip its query ends until the call
-// returns, and a lane whose query outlives the call holds its walk in its
-// own registers until its wave calls again: configs[4]'s node steps ran with
-// 31.5 of 64 lanes, its leaf passes with 18.9 (profiles/r05).  Here a walk
-// that outlives the call is parked in LDS -- the query's whole state, one
-// slot per owning lane of the block (threadIdx.x), its stack entries staying
-// where they are (the owner wave's stack region) -- and any lane of the
-// block whose own query is parked (or that has none) takes parked walks
-// from the pool, in the call and whenever it goes idle inside one, and
-// writes each finished walk's (t, id) into the owner's result slot.  A walk's
-// result does not depend on which lane steps it, nor in how many calls: the
-// nearest distance is a minimum with ties to the highest index, the any-hit
-// any occluder, and every trip is the one wide_walk would take from the same
-// state.  The owner picks its result up after a call (shading only its own
-// lanes, as before).
-//
-// LDS, after the stacks (pool_bytes): three planes of 16 B per slot (origin
-// + t, direction, (node + 1) << 8 | mask / sp | shadow << 8 / pend / pend2),
-// bpos, the result (t, id; id = POOL_SENT while pending), and 33 words of
-// flags: bit o of word o >> 5 = slot o parked, bit w of word 32 = word w
-// may be non-zero (set after the word's bit; a claimer that empties a word
-// clears its summary bit, then re-reads the word and sets it again if a
-// push came in between).
-constexpr int POOL_SLOTS = 1024;
-constexpr int POOL_SENT = (int)0x80000000;
-__host__ __device__ constexpr size_t pool_bytes() { return (size_t)POOL_SLOTS * (3 * 16 + 4 + 8) + 64 * 4; }
-struct WidePool {
-    uint4 *p0, *p1, *p2;
-    int *pb;
-    uint2 *res;
-    unsigned *bits;
-};
-__device__ __forceinline__ WidePool pool_carve(char *base)
-{
-    WidePool P;
-    P.p0 = (uint4 *)base;
-    P.p1 = P.p0 + POOL_SLOTS;
-    P.p2 = P.p1 + POOL_SLOTS;
-    P.pb = (int *)(P.p2 + POOL_SLOTS);
-    P.res = (uint2 *)(P.pb + POOL_SLOTS);
-    P.bits = (unsigned *)(P.res + POOL_SLOTS);
-    return P;
-}
-// Position of the r-th (from 0) set bit of v (r < popcount(v)).
-__device__ __forceinline__ int nth_set_bit(unsigned v, int r)
-{
-    int pos = 0;
-#pragma unroll
-    for (int sz = 16; sz >= 1; sz >>= 1) {
-        const unsigned lo = v & ((1u << sz) - 1u);
-        const int c = __builtin_popcount(lo);
-        if (r >= c) {
-            r -= c;
-            v >>= sz;
-            pos += sz;
-        } else {
-            v = lo;
-        }
-    }
-    return pos;
-}
-
-#ifndef RT_WIDE_POOL_REFILL
-#define RT_WIDE_POOL_REFILL 16   // pool walk: claim parked walks once >= REFILL/64 of the call's lanes are idle
-#endif
-
-// One pool call.  fresh: the lane starts a query of its own (W, r: as
-// wide_begin left them; its origin and direction already in its slot); the
-// other lanes of the call take parked walks.  Returns nothing: the owner
-// reads its result slot afterwards.  stk0 / sstride: the block's stack
-// region and one wave's share of it.  opts as wide_walk (budget, batch,
-// stop); refill (sflags bits 8..15): the idle share that triggers a claim.
-__device__ void wide_walk_pool(const BvhView &B, const uint4 *__restrict__ L, unsigned *__restrict__ stk0, int sstride,
-                               const WidePool &P, bool fresh, const ray3 &r, bool shadow0, BvhWalk &W, int opts,
-                               int refill)
-{
-    const int budget = (opts >> 8) & 255, batch = (opts >> 16) & 255, stop = (opts >> 24) & 255;
-    const int lane = threadIdx.x & 63;
-    int owner = fresh ? (int)threadIdx.x : -1;
-    v3 ro = r.o, rd = r.d;
-    float t = W.t;
-    int id = W.id, cur = W.node, pend = W.pend, pend2 = W.pend2, sp = W.sp, bpos = W.bpos;
-    unsigned m = W.m;
-    bool shadow = shadow0;
-    float ix, iy, iz, alpha;
-    int oct;
-    unsigned *my = stk0 + (threadIdx.x >> 6) * sstride + lane;
-    const auto derive = [&]() {
-        const float dx = fabsf(rd.x) < 1e-30f ? copysignf(1e-30f, rd.x) : rd.x;
-        const float dy = fabsf(rd.y) < 1e-30f ? copysignf(1e-30f, rd.y) : rd.y;
-        const float dz = fabsf(rd.z) < 1e-30f ? copysignf(1e-30f, rd.z) : rd.z;
-        ix = __builtin_amdgcn_rcpf(dx);
-        iy = __builtin_amdgcn_rcpf(dy);
-        iz = __builtin_amdgcn_rcpf(dz);
-        const float e = fabsf(rd.x * rd.x + rd.y * rd.y + rd.z * rd.z - 1.f);
-        alpha = e < 0x1p-16f ? BVH_K * (1.04e-3f + __builtin_amdgcn_sqrtf(e + 0x1p-22f)) : 1e30f;
-        oct = (dx < 0.f ? 1 : 0) | (dy < 0.f ? 2 : 0) | (dz < 0.f ? 4 : 0);
-    };
-    derive();
-    const unsigned *Lw = (const unsigned *)L;
-    const int n0 = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true));   // lanes in this call
-    int trips = 0;
-    bool dry = false;                  // the last claim found the pool empty
-    int nb0 = 64;                      // lanes holding a walk after the first claim
-    WALK_PROF(W, 0);
-    while (true) {
-        // ---- claim parked walks for idle lanes (one flag word per claim)
-        const unsigned long long im = __builtin_amdgcn_ballot_w64(owner < 0);
-        if (im && (trips == 0 || 64 * __builtin_popcountll(im) >= refill * n0) && (!dry || (trips & 3) == 0)) {
-            const int lead = __builtin_ctzll(__builtin_amdgcn_read_exec());
-            unsigned got = 0;
-            int wd = 0;
-            if (lane == lead) {
-                const unsigned s = __hip_atomic_load(P.bits + 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (s) {
-                    // (the wave's own two words first, then round the block)
-                    const int st = 2 * (int)(threadIdx.x >> 6) & 31;
-                    wd = (__builtin_ctz((s >> st) | (s << ((32 - st) & 31))) + st) & 31;
-                    const unsigned cw = __hip_atomic_load(P.bits + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    const int want_n = __builtin_popcountll(im);
-                    const unsigned want = __builtin_popcount(cw) <= want_n ? cw
-                                                                          : cw & ((1u << nth_set_bit(cw, want_n)) - 1u);
-                    unsigned rest = 0;
-                    if (want) {
-                        const unsigned old = __hip_atomic_fetch_and(P.bits + wd, ~want, __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
-                        got = old & want;
-                        rest = old & ~want;
-                    }
-                    if (rest == 0) {
-                        __hip_atomic_fetch_and(P.bits + 32, ~(1u << wd), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (__hip_atomic_load(P.bits + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-                            __hip_atomic_fetch_or(P.bits + 32, 1u << wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                }
-            }
-            got = __builtin_amdgcn_readfirstlane(got);
-            wd = __builtin_amdgcn_readfirstlane(wd);
-            dry = got == 0;
-            if (got) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
-                if (owner < 0 && rank < __builtin_popcount(got)) {
-                    const int o = 32 * wd + nth_set_bit(got, rank);
-                    const uint4 a = P.p0[o], b = P.p1[o], c = P.p2[o];
-                    bpos = P.pb[o];
-                    ro = mk(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z));
-                    t = __uint_as_float(a.w);
-                    rd = mk(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z));
-                    id = (int)b.w;
-                    cur = (int)(c.x >> 8) - 1;
-                    m = c.x & 255u;
-                    sp = (int)(c.y & 255u);
-                    shadow = (c.y >> 8) & 1u;
-                    pend = (int)c.z;
-                    pend2 = (int)c.w;
-                    owner = o;
-                    my = stk0 + (o >> 6) * sstride + (o & 63);
-                    derive();
-                }
-            }
-        }
-        const bool busy = owner >= 0;
-        const unsigned long long bm = __builtin_amdgcn_ballot_w64(busy);
-        if (!bm) break;                 // nothing held, nothing claimed
-        if (trips == 0) nb0 = __builtin_popcountll(bm);
-        const float maxt = t;           // (any hit: t never changes; nearest: maxt unused)
-        if (busy && m != 0 && pend2 == 0) {
-            WALK_PROF(W, 1);
-            int cw;
-            if (cur < 0) {
-                cw = 0;
-                m = 0;
-            } else {
-                const int p = __builtin_ctz(m);
-                m &= m - 1;
-                cw = (int)Lw[cur * WIDE_WORDS + 8 + (p ^ oct)];
-            }
-            if (cw < 0) {
-                if (pend == 0) pend = ~cw;
-                else pend2 = ~cw;
-            } else {
-                ray3 rr;
-                rr.o = ro;
-                rr.d = rd;
-                const unsigned hm = wide_visit(L + 7 * cw, rr, ix, iy, iz, alpha, oct, shadow ? maxt : t);
-                if (hm) {
-                    if (m) {
-                        my[64 * sp] = ((unsigned)cur << 8) | m;
-                        sp++;
-                    }
-                    cur = cw;
-                    m = hm;
-                }
-            }
-            if (m == 0 && sp > 0) {
-                sp--;
-                const unsigned e2 = my[64 * sp];
-                cur = (int)(e2 >> 8);
-                m = e2 & 255u;
-            }
-        }
-        trips++;
-        const unsigned long long pm = __builtin_amdgcn_ballot_w64(busy && pend != 0);
-        const unsigned long long sm = __builtin_amdgcn_ballot_w64(busy && m != 0 && pend2 == 0);
-        // (refill > 64: claims at the call's start only, then wide_walk's stop rule)
-        const bool out = trips >= budget || ((dry || refill > 64) && 64 * __builtin_popcountll(pm | sm) <= stop * (refill > 64 ? nb0 : n0));
-        const bool leaves = pm != 0 && (sm == 0 || out || 64 * __builtin_popcountll(pm & ~sm) >= batch * __builtin_popcountll(pm | sm));
-        if (leaves && busy && pend != 0) {
-            WALK_PROF(W, 2);
-            const int f = pend & 0xffffff, c = pend >> 24, c4 = c < BVH_LEAF_MAX ? c : BVH_LEAF_MAX;
-            float4 g[BVH_LEAF_MAX];
-#pragma unroll
-            for (int q = 0; q < BVH_LEAF_MAX; q++) g[q] = B.geo[f + (q < c4 ? q : 0)];
-            float dq[BVH_LEAF_MAX];
-            bool bad = false;
-#pragma unroll
-            for (int q = 0; q < BVH_LEAF_MAX; q++) {
-                const float opx = g[q].x - ro.x, opy = g[q].y - ro.y, opz = g[q].z - ro.z;
-                const float bb = opx * rd.x + opy * rd.y + opz * rd.z;
-                const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g[q].w;
-                bad = bad || (q < c4 && fabsf(det) < 0x1p-96f);
-                const float sd = sqrt_nr(det);
-                const float t1 = bb - sd, t2 = bb + sd;
-                dq[q] = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
-            }
-            if (wave_any(bad)) {
-                ray3 rr;
-                rr.o = ro;
-                rr.d = rd;
-#pragma unroll
-                for (int q = 0; q < BVH_LEAF_MAX; q++) dq[q] = sphere_hit(g[q], rr);
-            }
-#pragma unroll
-            for (int q = 0; q < BVH_LEAF_MAX; q++) {
-                if (q < c4) {
-                    const float d = dq[q];
-                    if (shadow) {
-                        if (d < maxt) bpos = f + q;
-                    } else if (d < t) {
-                        t = d;
-                        bpos = f + q;
-                    } else if (d == t) {
-                        const int cur_id = bpos >= 0 ? B.id[bpos] : id;
-                        if (B.id[f + q] > cur_id) bpos = f + q;
-                    }
-                }
-            }
-            if (c > BVH_LEAF_MAX) {
-                pend = (f + BVH_LEAF_MAX) | ((c - BVH_LEAF_MAX) << 24);
-            } else {
-                pend = pend2;
-                pend2 = 0;
-            }
-            if (shadow && (id >= 0 || bpos >= 0)) {
-                m = 0;
-                sp = 0;
-                pend = pend2 = 0;
-            }
-        }
-        // ---- finished walks: the result to the owner's slot, the lane idle
-        if (busy && m == 0 && pend == 0) {
-            if (bpos >= 0) id = shadow ? 0x7fffffff : B.id[bpos];
-            P.res[owner] = make_uint2(__float_as_uint(t), (unsigned)id);
-            owner = -1;
-        }
-        if (out) break;
-    }
-    // ---- walks still held go back to the pool
-    if (owner >= 0) {
-        P.p0[owner] = make_uint4(__float_as_uint(ro.x), __float_as_uint(ro.y), __float_as_uint(ro.z), __float_as_uint(t));
-        P.p1[owner] = make_uint4(__float_as_uint(rd.x), __float_as_uint(rd.y), __float_as_uint(rd.z), (unsigned)id);
-        P.p2[owner] = make_uint4(((unsigned)(cur + 1) << 8) | m, (unsigned)sp | (shadow ? 256u : 0u), (unsigned)pend,
-                                 (unsigned)pend2);
-        P.pb[owner] = bpos;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __hip_atomic_fetch_or(P.bits + (owner >> 5), 1u << (owner & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_or(P.bits + 32, 1u << (owner >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1362,91 +972,42 @@ __device__ __forceinline__ bool leaf_coop(const BvhView &B, const ray3 &r, bool 
                 const int q = b + pos + j * G;
                 g[l][j] = B.geo[f[l] + (q < c[l] ? q : 0)];
             }
-        if constexpr (G == 8 && RT_SPT_COOP_LEAFALL) {   // (G = 4: two spheres per lane -- the leaf-by-leaf form, no spills)
-            // every leaf's distances first (independent: the lone heavy wave's
-            // issue overlaps them), one range check for all, then the updates
-            float d[NL][S];
+#pragma unroll
+        for (int l = 0; l < NL; l++) {
+            if (b >= c[l]) continue;
+            float d[S];
             bool bad = false;
-    #pragma unroll
-            for (int l = 0; l < NL; l++)
-    #pragma unroll
-                for (int j = 0; j < S; j++) {
-                    const float opx = g[l][j].x - r.o.x, opy = g[l][j].y - r.o.y, opz = g[l][j].z - r.o.z;
-                    const float bb = opx * r.d.x + opy * r.d.y + opz * r.d.z;
-                    const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g[l][j].w;
-                    bad = bad || (b + pos + j * G < c[l] && fabsf(det) < 0x1p-96f);
-                    const float sd = sqrt_nr(det);
-                    const float t1 = bb - sd, t2 = bb + sd;
-                    d[l][j] = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
-                }
+#pragma unroll
+            for (int j = 0; j < S; j++) {
+                const float opx = g[l][j].x - r.o.x, opy = g[l][j].y - r.o.y, opz = g[l][j].z - r.o.z;
+                const float bb = opx * r.d.x + opy * r.d.y + opz * r.d.z;
+                const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g[l][j].w;
+                bad = bad || (b + pos + j * G < c[l] && fabsf(det) < 0x1p-96f);
+                const float sd = sqrt_nr(det);
+                const float t1 = bb - sd, t2 = bb + sd;
+                d[j] = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
+            }
             if (wave_any(bad)) {
-    #pragma unroll
-                for (int l = 0; l < NL; l++)
-    #pragma unroll
-                    for (int j = 0; j < S; j++) d[l][j] = sphere_hit(g[l][j], r);
+#pragma unroll
+                for (int j = 0; j < S; j++) d[j] = sphere_hit(g[l][j], r);
             }
-    #pragma unroll
-            for (int l = 0; l < NL; l++)
-    #pragma unroll
-                for (int j = 0; j < S; j++)
-                    if (b + pos + j * G >= c[l]) d[l][j] = MISS;
-    #pragma unroll
-            for (int l = 0; l < NL; l++) {
-                if (b >= c[l]) continue;
-                if (LOCAL && !shadow) {
-    #pragma unroll
-                    for (int j = 0; j < S; j++) {
-                        const int q = f[l] + b + pos + j * G;
-                        if (d[l][j] < t) {
-                            t = d[l][j];
-                            bpos = q;
-                        } else if (d[l][j] == t) {          // (d finite: a tie)
-                            const int cur_id = bpos >= 0 ? B.id[bpos] : id;
-                            if (B.id[q] > cur_id) bpos = q;
-                        }
-                    }
-                } else if (leaf_apply<COUNT, G>(B, shadow, maxt, f[l], b, pos, gbase, d[l], t, bpos, id)) {
-                    return true;
-                }
-            }
-        } else {
-    #pragma unroll
-            for (int l = 0; l < NL; l++) {
-                if (b >= c[l]) continue;
-                float d[S];
-                bool bad = false;
-    #pragma unroll
+#pragma unroll
+            for (int j = 0; j < S; j++)
+                if (b + pos + j * G >= c[l]) d[j] = MISS;
+            if (LOCAL && !shadow) {
+#pragma unroll
                 for (int j = 0; j < S; j++) {
-                    const float opx = g[l][j].x - r.o.x, opy = g[l][j].y - r.o.y, opz = g[l][j].z - r.o.z;
-                    const float bb = opx * r.d.x + opy * r.d.y + opz * r.d.z;
-                    const float det = bb * bb - (opx * opx + opy * opy + opz * opz) + g[l][j].w;
-                    bad = bad || (b + pos + j * G < c[l] && fabsf(det) < 0x1p-96f);
-                    const float sd = sqrt_nr(det);
-                    const float t1 = bb - sd, t2 = bb + sd;
-                    d[j] = t1 > EPS ? t1 : (t2 > EPS ? t2 : MISS);
-                }
-                if (wave_any(bad)) {
-    #pragma unroll
-                    for (int j = 0; j < S; j++) d[j] = sphere_hit(g[l][j], r);
-                }
-    #pragma unroll
-                for (int j = 0; j < S; j++)
-                    if (b + pos + j * G >= c[l]) d[j] = MISS;
-                if (LOCAL && !shadow) {
-    #pragma unroll
-                    for (int j = 0; j < S; j++) {
-                        const int q = f[l] + b + pos + j * G;
-                        if (d[j] < t) {
-                            t = d[j];
-                            bpos = q;
-                        } else if (d[j] == t) {             // (d finite: a tie)
-                            const int cur_id = bpos >= 0 ? B.id[bpos] : id;
-                            if (B.id[q] > cur_id) bpos = q;
-                        }
+                    const int q = f[l] + b + pos + j * G;
+                    if (d[j] < t) {
+                        t = d[j];
+                        bpos = q;
+                    } else if (d[j] == t) {             // (d finite: a tie)
+                        const int cur_id = bpos >= 0 ? B.id[bpos] : id;
+                        if (B.id[q] > cur_id) bpos = q;
                     }
-                } else if (leaf_apply<COUNT, G>(B, shadow, maxt, f[l], b, pos, gbase, d, t, bpos, id)) {
-                    return true;
                 }
+            } else if (leaf_apply<COUNT, G>(B, shadow, maxt, f[l], b, pos, gbase, d, t, bpos, id)) {
+                return true;
             }
         }
     }
@@ -1475,7 +1036,6 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
     const int pos = threadIdx.x & (G - 1), gbase = threadIdx.x & (64 - G);
     const int n0 = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true));
     int trips = 0;
-#if RT_SPT_COOP_LEAN
     // One trip as straight-line selects: the next child's word and the
     // stack top are read together at the trip's start (the pop can only
     // need the entry below the current top: a trip that descends does not
@@ -1483,9 +1043,10 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
     // masks its result), and only the leaf passes sit behind a wave-uniform
     // branch.  The old form's per-group branches cost the lone heavy wave
     // ~40 exec-mask and branch instructions per trip (c4_coop_phase_n8_spread.log).
-    // (RT_SPT_COOP_LOCAL, nearest hits: t / bpos are the lane's own best;
-    // tg, the group's minimum, is the culling limit)
-    constexpr bool LOC = G == 8 && RT_SPT_COOP_LOCAL;
+    // (G = 8, nearest hits: t / bpos are the lane's own best -- reduced to
+    // the group's culling limit tg once per leaf section and to the result
+    // once per query instead of per leaf: N = 8 / 4 shares -2 to -3 %)
+    constexpr bool LOC = G == 8;
     float tg = LOC ? grp_min<G>(t) : t;
     while (true) {
         const bool has = m != 0;
@@ -1556,90 +1117,6 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
         const unsigned long long am = __builtin_amdgcn_ballot_w64(m != 0);
         if (am == 0 || trips >= budget || 64 * __builtin_popcountll(am) <= stop * n0) break;
     }
-#else
-    while (true) {
-        if (m != 0) {
-            int cw;
-            if (cur < 0) {
-                cw = 0;
-                m = 0;
-            } else {
-                const int p = __builtin_ctz(m);
-                m &= m - 1;
-                cw = (int)Lw[cur * WIDE_WORDS + 8 + (p ^ oct)];
-            }
-            if (cw < 0) {                       // (a root leaf: child leaves are tested at their parent)
-                const int lf = ~cw;
-                const int fa[1] = {lf & 0xffffff}, ca[1] = {lf >> 24};
-                if (leaf_coop<COUNT, G, 1>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id)) {
-                    m = 0;
-                    sp = 0;
-                }
-            } else {
-                unsigned lm;
-                const unsigned hm =
-                    COUNT ? wide_visit_coop<G>(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase,
-                                               lm, Lmax + 8 * cw, shadow ? id : -1)
-                          : wide_visit_coop<G>(L + 7 * cw, r, ix, iy, iz, alpha, oct, shadow ? maxt : t, pos, gbase,
-                                               lm);
-                // The node's crossed leaves at once, RT_SPT_COOP_NL per pass
-                // (their words read and their sphere loads issued together),
-                // before its inner children.
-                bool occl = false;
-                unsigned l = lm;
-#ifdef RT_SPT_TRACE
-                const unsigned long long tr_l0 = l ? __builtin_amdgcn_s_memtime() : 0ull;
-#endif
-                while (l) {
-                    int fa[RT_SPT_COOP_NL], ca[RT_SPT_COOP_NL];
-#pragma unroll
-                    for (int q = 0; q < RT_SPT_COOP_NL; q++) {
-                        fa[q] = ca[q] = 0;
-                        if (l) {
-                            const int iq = __builtin_ctz(l);
-                            l &= l - 1;
-                            const int wq = ~(int)Lw[cw * WIDE_WORDS + 8 + (iq ^ oct)];
-                            fa[q] = wq & 0xffffff;
-                            ca[q] = wq >> 24;
-                        }
-                    }
-#ifdef RT_SPT_TRACE
-                    W.tr_leafruns++;
-#endif
-                    if (leaf_coop<COUNT, G, RT_SPT_COOP_NL>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id)) {
-                        occl = true;
-                        break;
-                    }
-                }
-#ifdef RT_SPT_TRACE
-                if (lm) W.tr_leaf += (unsigned)(__builtin_amdgcn_s_memtime() - tr_l0);
-#endif
-                const unsigned nm = hm & ~lm;
-                if (occl) {
-                    m = 0;
-                    sp = 0;
-                } else if (nm) {
-                    if (m) {
-                        my[64 * sp] = ((unsigned)cur << 8) | m;
-                        sp++;
-                    }
-                    cur = cw;
-                    m = nm;
-                }
-            }
-            if (m == 0 && sp > 0) {
-                sp--;
-                const unsigned e2 = my[64 * sp];
-                cur = (int)(e2 >> 8);
-                m = e2 & 255u;
-            }
-        }
-        trips++;
-        const unsigned long long am = __builtin_amdgcn_ballot_w64(m != 0);
-        if (am == 0 || trips >= budget || 64 * __builtin_popcountll(am) <= stop * n0) break;
-    }
-#endif
-#if RT_SPT_COOP_LEAN
     if (LOC && m == 0 && !shadow) {
         // the group's result from its lanes' bests: the minimum distance,
         // ties to the highest reference index (bpos -1: the query's first id)
@@ -1656,7 +1133,6 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
         t = tf;
         bpos = wb;
     }
-#endif
 #ifdef RT_SPT_TRACE
     W.tr_trips += trips;
 #endif
@@ -1708,6 +1184,174 @@ __device__ uint4 *g_spt_trace;
 __device__ int g_spt_only_group = -1;
 #endif
 
+// ---------------------------------------------------------------------------
+// Split walk / shade (WS): the 8-wide kernels with warp-specialised waves.
+//
+// In the one-role kernel every lane owns one pixel and walks its own queries:
+// configs[4]'s node steps ran with 31.5 of 64 lanes and its leaf passes with
+// 18.9 (profiles/r05), because a wave's lanes need different numbers of
+// trips, and a walk can only be continued by the lane that owns its pixel's
+// path state.  Here the block's waves take one of two roles:
+//   * shader waves (waves nwalk..15) each hold a pixel per lane -- its RNG
+//     words, accumulator and path state in VGPRs, as render_kernel's loop --
+//     and, where that loop walks, post the query into the lane's LDS slot
+//     and wait for its result;
+//   * walker waves (waves 0..nwalk-1, one per SIMD at nwalk = 4) claim posted
+//     queries, walk them (wide_walk: the same trips, the same float
+//     operations), write each result into its slot and claim the next query
+//     as soon as a lane is free.
+// With 12 shader waves there are 768 queries in flight per CU for 256 walker
+// lanes, so a walker lane that finishes finds another query waiting: node
+// steps and leaf passes run with (nearly) full waves however the trip
+// counts differ.  Results are the reference's: a query's result (nearest
+// distance, highest index on ties; or "some occluder") does not depend on
+// which lane walks it, and each pixel still runs its own samples, draws and
+// float operations in order -- only the lane that tests its spheres changes.
+//
+// LDS after the nodes and stacks (ws_bytes): per shader slot the query
+// (origin + t on entry, direction + shadow flag: 32 B) and its result (t, id:
+// 8 B; id = WS_SENT while pending), then one ready bit per slot (posted, not
+// yet claimed: 2 words per shader wave) and a control word (shader waves
+// still running).  Hand-offs are LDS-only: plain stores, a workgroup-scope
+// release, a bit set by atomic OR; claims by atomic AND, a workgroup-scope
+// acquire; results by one 64-bit store the owner polls.
+constexpr int WS_SENT = (int)0x80000000;
+__host__ __device__ constexpr size_t ws_bytes(int nslots) { return (size_t)nslots * 40 + (size_t)(nslots / 32) * 4 + 16; }
+struct WsLds {
+    float4 *qo, *qd;        // per slot: origin.xyz, t on entry | direction.xyz, shadow (0 / 1)
+    unsigned long long *qr; // per slot: result t bits | id << 32 (id = WS_SENT: pending)
+    unsigned *ready;        // nslots / 32 words
+    int *ctl;               // [0]: shader waves still running, [1]: abort (a spin ran past its bound)
+};
+__device__ __forceinline__ WsLds ws_carve(char *base, int nslots)
+{
+    WsLds Q;
+    Q.qo = (float4 *)base;
+    Q.qd = Q.qo + nslots;
+    Q.qr = (unsigned long long *)(Q.qd + nslots);
+    Q.ready = (unsigned *)(Q.qr + nslots);
+    Q.ctl = (int *)(Q.ready + nslots / 32);
+    return Q;
+}
+// Position of the r-th (from 0) set bit of v (r < popcount(v)).
+__device__ __forceinline__ int nth_set_bit(unsigned v, int r)
+{
+    int pos = 0;
+#pragma unroll
+    for (int sz = 16; sz >= 1; sz >>= 1) {
+        const unsigned lo = v & ((1u << sz) - 1u);
+        const int c = __builtin_popcount(lo);
+        if (r >= c) {
+            r -= c;
+            v >>= sz;
+            pos += sz;
+        } else {
+            v = lo;
+        }
+    }
+    return pos;
+}
+// Spin bound of every WS wait (s_sleep 1 per poll: ~seconds): past it the
+// block aborts -- a wrong frame and a flagged error (counters[... ] is not
+// touched; the host sees it through ws_abort) instead of a hung GPU.
+constexpr unsigned WS_SPIN_MAX = 1u << 24;
+
+// s_setprio with a run-time level (the instruction takes an immediate).
+__device__ __forceinline__ void set_prio(int p)
+{
+    if (p == 3) __builtin_amdgcn_s_setprio(3);
+    else if (p == 2) __builtin_amdgcn_s_setprio(2);
+    else if (p == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
+// The walker role.  opts: wide_walk's budget / batch / stop (bits 8..31 as
+// render_kernel's split); nwords: ready words (shader slots / 32).
+__device__ void ws_walker(const BvhView &B, const uint4 *__restrict__ L, unsigned *__restrict__ stk, const WsLds &Q,
+                          int nwords, int opts, int *abort_flag)
+{
+    const int lane = threadIdx.x & 63;
+    int slot = -1;
+    ray3 r;
+    bool shadow = false;
+    BvhWalk W;
+#ifdef RT_SPT_PROF
+    for (int b = 0; b < 3; b++) W.pf_l[b] = W.pf_w[b] = 0;
+#endif
+#ifdef RT_SPT_TRACE
+    W.tr_leaf = W.tr_trips = W.tr_leafruns = 0;
+#endif
+    int scan = (int)(threadIdx.x >> 6) * 5 % nwords;   // (walker waves start their claims on different words)
+    unsigned spins = 0;
+    while (true) {
+        // ---- idle lanes claim posted queries: one ready word per round, up
+        // to two rounds (its lanes rank themselves among the idle ones)
+#pragma unroll 1
+        for (int round = 0; round < 2; round++) {
+            const unsigned long long im = __builtin_amdgcn_ballot_w64(slot < 0);
+            if (!im) break;
+            const unsigned v = lane < nwords ? __hip_atomic_load(Q.ready + lane, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
+            const unsigned long long nz = __builtin_amdgcn_ballot_w64(v != 0u);
+            if (!nz) break;
+            // the first non-empty word at or after `scan`
+            const unsigned long long rot = (nz >> scan) | (scan ? nz << (64 - scan) : 0ull);
+            const int wd = (__builtin_ctzll(rot) + scan) % 64;
+            scan = (wd + 1) % nwords;
+            const unsigned cw = __builtin_amdgcn_readlane(v, wd);
+            const int want = __builtin_popcountll(im);
+            const unsigned take = __builtin_popcount(cw) <= want ? cw : cw & ((1u << nth_set_bit(cw, want)) - 1u);
+            unsigned got = 0;
+            if (lane == __builtin_ctzll(__builtin_amdgcn_read_exec()))
+                got = __hip_atomic_fetch_and(Q.ready + wd, ~take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & take;
+            got = __builtin_amdgcn_readfirstlane(got);
+            if (!got) continue;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
+            if (slot < 0 && rank < __builtin_popcount(got)) {
+                slot = 32 * wd + nth_set_bit(got, rank);
+                const float4 a = Q.qo[slot], b = Q.qd[slot];
+                r.o = mk(a.x, a.y, a.z);
+                r.d = mk(b.x, b.y, b.z);
+                shadow = __float_as_int(b.w) != 0;
+                wide_begin<false>(B, r, shadow, a.w, W);
+            }
+        }
+        const unsigned long long bm = __builtin_amdgcn_ballot_w64(slot >= 0);
+        if (!bm) {
+            if (__hip_atomic_load(Q.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) break;
+            if (++spins > WS_SPIN_MAX || __hip_atomic_load(Q.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                if (lane == 0) {
+                    __hip_atomic_store(Q.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    atomicAdd(abort_flag, 1);
+                }
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        spins = 0;
+        if (slot >= 0) {
+            const bool done = wide_walk<false>(B, L, stk, r, shadow, W, opts);
+            if (done) {
+                const unsigned long long res = (unsigned long long)__float_as_uint(W.t) |
+                                               ((unsigned long long)(unsigned)W.id << 32);
+                __hip_atomic_store(Q.qr + slot, res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                slot = -1;
+            }
+        }
+    }
+#ifdef RT_SPT_PROF
+    for (int b = 0; b < 3; b++) {   // walker lanes / wave-executions of calls, node steps, leaf passes
+        const unsigned long long l = wave_sum_u64(W.pf_l[b]), v = wave_sum_u64(W.pf_w[b]);
+        if (lane == 0) {
+            atomicAdd(&g_spt_prof[2 * (PB_WCALL + b)], l);
+            atomicAdd(&g_spt_prof[2 * (PB_WCALL + b) + 1], v);
+        }
+    }
+#endif
+}
+
 // toInt, vec.h:62 (clamp macro keeps -0.0; glibc powf via rt_glibc_math.h).
 __device__ __forceinline__ int to_int(float x)
 {
@@ -1715,63 +1359,19 @@ __device__ __forceinline__ int to_int(float x)
     return (int)(rtm::powf(c, 1.f / 2.2f) * 255.f + .5f);
 }
 
-#ifndef RT_SPT_QV
-#define RT_SPT_QV 2         // sphere query form: 2 = query_bf, 1 = query (A/B builds)
-#endif
-#ifndef RT_SPT_QUNROLL
-#define RT_SPT_QUNROLL 3
-#endif
-#ifndef RT_SPT_PRIO
-#define RT_SPT_PRIO 1       // progress-levelled s_setprio (A/B: 0 = off)
-#endif
-#ifndef RT_SPT_MINWAVES
-#define RT_SPT_MINWAVES 1   // __launch_bounds__ min waves per SIMD (occupancy A/B builds)
-#endif
-#ifndef RT_BVH_MINWAVES
-#define RT_BVH_MINWAVES 6   // the hierarchy (GEO_BVH) kernels: 93 -> 80 VGPRs (2 spilled), occupancy 5 -> 6: the
-                            // latency-bound walk gains more from the sixth wave than the spills cost (-10 %)
-#endif
+// Occupancy of the kernel variants (__launch_bounds__ minimum waves per
+// SIMD; every bound measured against its neighbours):
+//   full-scan one-query kernels: unbounded (1);
+//   the uncounted two-query kernel (DUAL): 7 -- 85 -> 72 VGPRs, no VGPR
+//     spills, occupancy 5 -> 7: Cornell 1080p 17.87 -> 17.3 ms;
+//   binary-hierarchy (GEO_BVH) kernels: 6 -- 93 -> 80 VGPRs (2 spilled): the
+//     latency-bound walk gains more from the sixth wave than the spills cost;
+//   8-wide (GEO_WIDE) kernels: 4 -- 126 VGPRs unbounded; 5 or 6 spill;
+//   counted hierarchy kernels (not timed): 4, room for the counters.
+constexpr int SPT_MINWAVES = 1, SPT_DUAL_MINWAVES = 7, BVH_MINWAVES = 6, WIDE_MINWAVES = 4, BVH_MINWAVES_COUNT = 4;
 constexpr int GEO_LDS = 0, GEO_GLOBAL = 1, GEO_BVH = 2, GEO_WIDE = 3;
-#ifndef RT_WIDE_PERSIST
-#define RT_WIDE_PERSIST 1   // 8-wide kernels: persistent waves taking tiles from a work counter (A/B: 0 = a wave per tile)
-#endif
-#ifndef RT_WIDE_MINWAVES
-#define RT_WIDE_MINWAVES 4  // the 8-wide (LDS) hierarchy kernels: 126 VGPRs unbounded; 5 or 6 waves per SIMD spill
-#endif
-#ifndef RT_SPT_COOP_G
-#define RT_SPT_COOP_G 8     // lanes per pixel of the cooperative walk in windows of <= 5 waves per SIMD (8 or 4;
-                            // windows of 5..10 use 4, launch())
-#endif
-#ifndef RT_WIDE_SPREAD
-#define RT_WIDE_SPREAD 1    // 8-wide persistent kernels: first tier-1 sub-items assigned wave-major (A/B: 0)
-#endif
-#ifndef RT_WIDE_POOL
-#define RT_WIDE_POOL 0      // uncounted 8-wide kernels: the block pool of parked walks (wide_walk_pool; A/B:
-                            // exact, configs[4] 24.3 -> 32.8 ms at its best setting, profiles/r05/c4_walk_pool_ab.log)
-#endif
-#ifndef RT_SPT_REFILL
-#define RT_SPT_REFILL 0    // 8-wide persistent kernels: a lane whose pixel is done takes the next pixel (A/B: 1;
-                            // 2: not in waves that started on a routed heavy tile)
-#endif
-#ifndef RT_SPT_REFILL_COUNT
-#define RT_SPT_REFILL_COUNT 1   // ... and in the full-counter 8-wide kernel (configs[4] counted 60-61 -> 51 ms: its
-                                // highest-occluder shadow walks spread a tile's pixel durations; A/B: 0)
-#endif
-#ifndef RT_SPT_REFILL_BATCH
-#define RT_SPT_REFILL_BATCH 1   // refill once this many lanes are free (or no lane of the wave has a pixel)
-#endif
-#ifndef RT_SPT_GSTORE
-#define RT_SPT_GSTORE 1     // hierarchy kernels: a group's outputs stored whole by its last wave (A/B: 0)
-#endif
-constexpr int GS_BYTES = 6160;      // per tile group: 8 x 96 colour floats, 8 x 64 seed words, 8 x 32 pixels, count
+constexpr int GS_BYTES = 6160;      // GEO_BVH group staging strip: 8 x 96 colour floats, 8 x 64 seed words, 8 x 32 pixels, count
 
-#ifndef RT_SPT_DUAL_MINWAVES
-#define RT_SPT_DUAL_MINWAVES 7   // the uncounted two-query kernel: 85 -> 72 VGPRs (no VGPR spills; a few SGPRs spill
-                                 // to VGPR lanes), occupancy 5 -> 7: Cornell 1080p 17.87 -> 17.3 ms
-#endif
-#ifndef RT_BVH_MINWAVES_COUNT
-#define RT_BVH_MINWAVES_COUNT 4   // the counted hierarchy kernels (not timed): room for the counters, no spills
-#endif
 // DUAL (path tracing, full-scan geometry, scenes with exactly one light): a
 // DIFF vertex builds its light sample's shadow ray AND its bounce ray in the
 // same iteration -- SampleLights' draws do not depend on the shadow test, so
@@ -1786,10 +1386,16 @@ constexpr int GS_BYTES = 6160;      // per tile group: 8 x 96 colour floats, 8 x
 // CG (8-wide kernels): lanes per pixel of the cooperative walk this kernel
 // carries (8 or 4), or 0 -- no cooperative code (windows without a
 // cooperative tier: the full frame, N = 2 shares).
-template <bool DL, bool COUNT, int GEO, bool DUAL = false, bool RAYS = false, int CG = 0>
-__global__ void __launch_bounds__(1024, GEO == 2 ? ((COUNT || RAYS) ? RT_BVH_MINWAVES_COUNT : RT_BVH_MINWAVES)
-                                              : GEO == 3 ? ((COUNT || RAYS) ? RT_BVH_MINWAVES_COUNT : RT_WIDE_MINWAVES)
-                                              : ((DUAL && !COUNT && !RAYS) ? RT_SPT_DUAL_MINWAVES : RT_SPT_MINWAVES))
+// WS (8-wide, uncounted or rays-only, CG = 0): split walk / shade roles
+// (ws_walker above); wsopt bits 0..3 = walker waves, 4..5 = their issue
+// priority, 8..31 = their wide_walk options (as split); sflags bits 8..15 =
+// the share of a shader wave's waiting lanes (in 1/64) whose results it
+// waits for before it shades, 16..23 = the most polls it waits for them,
+// 24..25 = the shader waves' issue priority.
+template <bool DL, bool COUNT, int GEO, bool DUAL = false, bool RAYS = false, int CG = 0, bool WS = false>
+__global__ void __launch_bounds__(1024, GEO == 2 ? ((COUNT || RAYS) ? BVH_MINWAVES_COUNT : BVH_MINWAVES)
+                                              : GEO == 3 ? ((COUNT || RAYS) ? BVH_MINWAVES_COUNT : WIDE_MINWAVES)
+                                              : ((DUAL && !COUNT && !RAYS) ? SPT_DUAL_MINWAVES : SPT_MINWAVES))
 render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam,
               float *__restrict__ colors, const uint32_t *seeds_in,
               uint32_t *seeds_out, uint32_t *__restrict__ pixels, int w, int h,
@@ -1798,14 +1404,14 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
               const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
               const float4 *__restrict__ g_col, const float4 *__restrict__ g_lrec, int nlights,
               BvhView bvh, unsigned long long *__restrict__ counters, int *__restrict__ work, int split,
-              int nheavy, int sflags)
+              int nheavy, int sflags, int wsopt)
 {
     constexpr bool LDS = GEO == GEO_LDS;
     // GEO_WIDE: persistent waves -- each wave takes 8x8 tiles from a work
     // counter (in the adaptive order's slot sequence, heaviest groups first)
     // until the window is done, so a block's LDS copy of the hierarchy is
     // made once and a CU never idles behind one block's slowest wave.
-    constexpr bool PERSIST = GEO == GEO_WIDE && RT_WIDE_PERSIST;
+    constexpr bool PERSIST = GEO == GEO_WIDE;
     // Dynamic LDS carve (16-B multiples): geo | emi | col (n each) | lrec (3 per light),
     // a copy of the scene's global SoA (spt_scene_create).
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1826,13 +1432,6 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // block its lanes' stacks ((wdepth - 1) entries x 64 lanes x 4 B).
     const uint4 *wL = (const uint4 *)smem;
     unsigned *wstk = nullptr;
-    // RT_WIDE_POOL (uncounted kernels, sflags bit 1): the block's pool of
-    // parked walks (wide_walk_pool) after the stacks.
-    constexpr bool POOLED = GEO == GEO_WIDE && !COUNT && RT_WIDE_POOL;
-    const int wsstride = 64 * (bvh.wdepth > 1 ? bvh.wdepth - 1 : 1);
-    WidePool wpool = {};
-    if (POOLED)
-        wpool = pool_carve(smem + (size_t)112 * bvh.wnodes + (size_t)(blockDim.x >> 6) * 4 * wsstride);
     if (GEO == GEO_WIDE) {
         uint4 *d = (uint4 *)smem;
         for (int i = threadIdx.x; i < 7 * bvh.wnodes; i += blockDim.x) d[i] = bvh.wnode[i];
@@ -1840,9 +1439,27 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             for (int i = threadIdx.x; i < 2 * bvh.wnodes; i += blockDim.x) d[7 * bvh.wnodes + i] = bvh.wmax[i];
         wstk = (unsigned *)(smem + (size_t)(COUNT ? 144 : 112) * bvh.wnodes) +
                (size_t)(threadIdx.x >> 6) * 64 * (bvh.wdepth - 1);
-        if (POOLED && (sflags & 2))
-            for (int i = threadIdx.x; i < 33; i += blockDim.x) wpool.bits[i] = 0u;
-        __syncthreads();
+    }
+    // WS: the query slots after every wave's stack, ready words and control
+    // zeroed (ctl[0] = the shader waves) before the barrier.
+    const int nwalk = WS ? (wsopt & 15) : 0;
+    WsLds wsq = {};
+    if constexpr (WS) {
+        const int nslot = ((int)(blockDim.x >> 6) - nwalk) * 64;
+        wsq = ws_carve(smem + (size_t)112 * bvh.wnodes + (size_t)(blockDim.x >> 6) * 256 * (bvh.wdepth - 1), nslot);
+        for (int i = threadIdx.x; i < nslot / 32; i += blockDim.x) wsq.ready[i] = 0u;
+        if (threadIdx.x == 0) {
+            wsq.ctl[0] = (int)(blockDim.x >> 6) - nwalk;
+            wsq.ctl[1] = 0;
+        }
+    }
+    if (GEO == GEO_WIDE) __syncthreads();
+    if constexpr (WS) {
+        if ((int)(threadIdx.x >> 6) < nwalk) {            // the walker role, for the whole launch
+            set_prio((wsopt >> 4) & 3);
+            ws_walker(bvh, wL, wstk, wsq, ((int)(blockDim.x >> 6) - nwalk) * 2, wsopt & ~255, work + 3);
+            return;
+        }
     }
 
     // 8x8 pixel tiles of the row window, one per wave, in groups of four
@@ -1888,8 +1505,8 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // wave then takes the rest in order (work[0]).
     // (by the wave's first active lane: refill claims fetch from inside the
     // pixel loop, where lanes that ran out of work have left)
-    // (RT_WIDE_SPREAD below: the first min(hw, waves per block) x #blocks tier-1 sub-items are assigned statically)
-    const int nstatic = (PERSIST && RT_WIDE_SPREAD) ? min(min(hw, (int)(blockDim.x >> 6)) * (int)gridDim.x, n1 << hs) : 0;
+    // (below: the first min(hw, waves per block) x #blocks tier-1 sub-items are assigned statically)
+    const int nstatic = PERSIST ? min(min(hw, (int)(blockDim.x >> 6)) * (int)gridDim.x, n1 << hs) : 0;
     const auto fetch = [&]() {
         int v = 0;
         if (lane == __builtin_ctzll(__builtin_amdgcn_read_exec())) {
@@ -1908,24 +1525,24 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     };
     int f = ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) * 4 + (wave & 3);
     if (PERSIST) {
-        // RT_WIDE_SPREAD: the first tier-1 sub-item of wave w of block b is
+        // The first tier-1 sub-item of wave w of block b is
         // w * #blocks + b, not the next one a shared counter hands out: the
         // heaviest tiles' sub-items (dispatch order) land one per CU, beside
         // lighter ones on their SIMD, where the counter gave a whole heavy
         // tile's rows to the waves of the first block to start.
         const int fs = wave * (int)gridDim.x + (int)blockIdx.x;
-        f = (RT_WIDE_SPREAD && wave < hw && fs < (n1 << hs)) ? fs : __builtin_amdgcn_readfirstlane(fetch());
+        f = (wave < hw && fs < (n1 << hs)) ? fs : __builtin_amdgcn_readfirstlane(fetch());
     }
     while (!PERSIST || f < nwork) {
     const bool heavy_ = f < (n1 << hs);
-    // hs = 3 (COOP, G = 8): a heavy tile's 8 sub-items are 8 rows of 8 pixels
-    // with eight lanes per pixel (lane group g = pixel g of the row), walking
-    // the hierarchy cooperatively (wide_walk_coop); hs = 2 with split bit 2
-    // (G = 4): 4 sub-items of 16 pixels, four lanes per pixel.  Otherwise a
-    // sub-item is 64 >> hs pixels, a lane each.
-    const int cg = (GEO == GEO_WIDE && CG != 0 && heavy_ && hs == (CG == 8 ? 3 : 2) && (split & 4)) ? CG : 0;
-    const bool coop = cg != 0;
-    const int sp_ = heavy_ && !coop ? hs : 0;
+    // Tier-1 (heavy) items are cooperative (the host sends them only to a
+    // kernel carrying the walk, CG != 0, with hs = log2(CG)): hs = 3 (G = 8):
+    // a heavy tile's 8 sub-items are 8 rows of 8 pixels with eight lanes per
+    // pixel (lane group g = pixel g of the row), walking the hierarchy
+    // cooperatively (wide_walk_coop); hs = 2 (G = 4): 4 sub-items of 16
+    // pixels, four lanes per pixel.
+    const bool coop = GEO == GEO_WIDE && CG != 0 && heavy_;
+    const int cg = coop ? CG : 0;
     const int item = heavy_ ? f >> hs : f - (n1 << hs) + n1;
     const int sub = heavy_ ? f & ((1 << hs) - 1) : 0;
     const int slot = item >> 2;
@@ -1935,15 +1552,14 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     const int grp = group_order ? (slot < nslots ? group_order[slot] : -1) : slot;
     const bool gvalid = (unsigned)grp < (unsigned)((ntiles + 3) >> 2);
     const int tile = grp * 4 + (item & 3);
-    const int li = coop ? (sub << (6 - hs)) + (cg == 8 ? lane >> 3 : lane >> 2)   // pixel of the 8x8 tile
-                        : (sub << (6 - sp_)) + lane;    //   (valid: lane < 64 >> split)
+    const int li = coop ? (sub << (6 - hs)) + (cg == 8 ? lane >> 3 : lane >> 2) : lane;   // pixel of the 8x8 tile
     const bool lead = !coop || (lane & (cg - 1)) == 0;  // the lane that stores the pixel and counts
     unsigned long long t_start = 0;
     if (SCHED) t_start = __builtin_amdgcn_s_memrealtime();
     // GSTORE (hierarchy kernels): per group of the block a 32x8 staging
     // strip in LDS -- colours, seeds, pixels -- and an arrival count.
     // (Addresses recomputed where used: held across the loop they spilled.)
-    constexpr bool GSTORE = GEO == GEO_BVH && RT_SPT_GSTORE;
+    constexpr bool GSTORE = GEO == GEO_BVH;
 #define GS_BASE() (smem + (size_t)((threadIdx.x >> 6) >> 2) * GS_BYTES)
     if (GSTORE) {
         if ((threadIdx.x & 255) == 0) *(int *)(GS_BASE() + 6144) = 0;
@@ -1953,7 +1569,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // gstride > 1: the window is every gstride-th 8-row group from row_begin
     // (spt_scene_render_groups_async, multi-GPU load balance).
     int y = row_begin + (tile / tiles_x) * 8 * gstride + (li >> 3);
-    // Refill (8-wide persistent kernels, items past the cooperative / split
+    // Refill (full-counter 8-wide kernels, items past the cooperative
     // tier): the wave starts on this item's 64 pixels, and from then on a
     // lane whose pixel has taken all its samples stores it and takes the next
     // pixel of the dispatch sequence (the rest of the wave's current item,
@@ -1962,19 +1578,20 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // beside the fractal): waiting for the tile's slowest pixel left 28 % of
     // the lanes idle (tools/c4_lanes.py).  Every pixel's computation is
     // unchanged -- only which lane runs it, and when.
-    // (The counted kernel refills by default: there the tile tail, not the
-    // levelling, dominates -- 28 of 64 lanes per iteration without refill,
-    // 52 with, profiles/r05/c4_counted_refill.log.)
-    constexpr int REFILL = (COUNT && RT_SPT_REFILL_COUNT && !RT_SPT_REFILL) ? 1 : RT_SPT_REFILL;
-    const bool refill = REFILL && PERSIST && !heavy_ && (REFILL == 1 || f >= (n1 << hs) + n2);
+    // Counted kernels only: there the tile tail, not the levelling,
+    // dominates -- 28 of 64 lanes per iteration without refill, 52 with,
+    // profiles/r05/c4_counted_refill.log; on the uncounted frame refill
+    // measured +7 % (its waves lose the levelled priority).
+    // (WS: the shader waves always refill -- a lane's pixel is its unit)
+    const bool refill = (COUNT || WS) && PERSIST && !heavy_;
 #ifdef RT_SPT_TRACE
-    bool active = gvalid && lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end &&
+    bool active = gvalid && tile < ntiles && x < w && y < row_end &&
                   (g_spt_only_group < 0 || grp == g_spt_only_group);
     unsigned tr_walk = 0, tr_leaf = 0, tr_trips = 0, tr_leafruns = 0, tr_queries = 0;
     const unsigned long long tr_c0 = __builtin_amdgcn_s_memtime();
     const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();
 #else
-    bool active = gvalid && lane < (64 >> sp_) && tile < ntiles && x < w && y < row_end;
+    bool active = gvalid && tile < ntiles && x < w && y < row_end;
 #endif
 
 #ifdef RT_SPT_TRACE
@@ -1998,7 +1615,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         bool px_ok = active, exhausted = false;
         int pgrp = grp;
         unsigned pix_t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
-        int rf_f = f, rf_p = 64 >> sp_;
+        int rf_f = f, rf_p = 64;
 
         // Per-lane path state.  Every loop iteration issues exactly ONE ray
         // query for every live lane -- the path ray (nearest hit) or, while a
@@ -2043,26 +1660,21 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
 #endif
         bool walking = false;  //   and whether it is suspended mid-walk
         constexpr float nc = 1.f, nt = 1.5f;
-#if RT_SPT_PRIO
         // prio_sched: the three level boundaries as fractions of the samples
-        // (8 bits each, in 1/256; host: prio_schedule).
-        // With an adaptive order, the first (prio_sched >> 24) * 16 group
-        // slots hold the heaviest groups: their waves keep the top priority
-        // throughout (they set the frame's critical path); the others level
-        // down from 2.
-        const bool heavy = SCHED && slot < ((prio_sched >> 24) & 255) * 16;
-        const bool top3 = !SCHED || heavy || (prio_sched >> 24) == 0;
-        int prio_level = 0, prio_next = heavy ? nsamples + 1 : (nsamples * (prio_sched & 255)) >> 8;
-        if (top3) __builtin_amdgcn_s_setprio(3);
-        else __builtin_amdgcn_s_setprio(2);
-#endif
+        // (8 bits each, in 1/256; host: prio_schedule).  Every wave starts at
+        // the top priority and levels down (no group is held at the top: the
+        // round-2 rule, measured best for the binary walk, cost configs[4]
+        // 2-8 % with the 8-wide one, profiles/r05/c4_heavy_prio_sweep.log).
+        int prio_level = 0, prio_next = (nsamples * (prio_sched & 255)) >> 8;
+        if (WS) set_prio((sflags >> 24) & 3);
+        else __builtin_amdgcn_s_setprio(3);
         while (true) {
             if (refill) {
                 // ---- refill: lanes whose pixel is done store it, then take
                 // the next pixels of the wave's dispatch sequence
                 const bool want = k >= nsamples && !exhausted;
                 const unsigned long long wm = __builtin_amdgcn_ballot_w64(want);
-                if (wm && (__builtin_popcountll(wm) >= RT_SPT_REFILL_BATCH || wm == __builtin_amdgcn_read_exec())) {
+                if (wm) {
                     if (want && px_ok) {
                         if (nsamples > 0) {
                             colors[3 * (size_t)i] = col.x;
@@ -2164,7 +1776,6 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 if (!refill || exhausted) break;
                 continue;                       // (a pixel past the frame's edge: claim again)
             }
-#if RT_SPT_PRIO
             // Progress-levelled issue priority.  The SIMD arbitrates VALU issue
             // by priority, then age, so waves that start together finish one
             // after another and the last one runs alone at a fraction of the
@@ -2175,11 +1786,10 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             if (!refill && !wave_any(k < prio_next)) {
                 prio_level++;
                 prio_next = prio_level < 3 ? (nsamples * ((prio_sched >> (8 * prio_level)) & 255)) >> 8 : nsamples;
-                if (prio_level == 1 && top3) __builtin_amdgcn_s_setprio(2);
-                else if ((prio_level == 2 && top3) || (prio_level == 1 && !top3)) __builtin_amdgcn_s_setprio(1);
+                if (prio_level == 1) __builtin_amdgcn_s_setprio(2);
+                else if (prio_level == 2) __builtin_amdgcn_s_setprio(1);
                 else __builtin_amdgcn_s_setprio(0);
             }
-#endif
 
             SPT_PROF(PB_ITER);
 #ifdef RT_SPT_TRACE
@@ -2237,45 +1847,67 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 const unsigned long long tr_w0 = __builtin_amdgcn_s_memtime();
                 tr_queries += !walking;
 #endif
-                if (POOLED && (sflags & 2) && !coop) {
-                    // Pooled: a new query starts here (its origin and
-                    // direction kept in its slot, its result pending); a
-                    // lane whose query is parked works on the pool instead.
-                    const int me = threadIdx.x;
+                if constexpr (WS) {
+                    // Post the query into this lane's slot (unless it is
+                    // waiting for one already), then wait -- asleep -- until
+                    // enough of the wave's waiting lanes have their results.
+                    const int me = (wave - nwalk) * 64 + lane;
                     if (!walking) {
-                        wide_begin<COUNT>(bvh, ray, shadow, t, walk);
-                        wpool.p0[me] = make_uint4(__float_as_uint(ray.o.x), __float_as_uint(ray.o.y),
-                                                  __float_as_uint(ray.o.z), 0u);
-                        wpool.p1[me] = make_uint4(__float_as_uint(ray.d.x), __float_as_uint(ray.d.y),
-                                                  __float_as_uint(ray.d.z), 0u);
-                        wpool.res[me] = make_uint2(0u, (unsigned)POOL_SENT);
+                        wsq.qo[me] = make_float4(ray.o.x, ray.o.y, ray.o.z, t);
+                        wsq.qd[me] = make_float4(ray.d.x, ray.d.y, ray.d.z, __int_as_float(shadow ? 1 : 0));
+                        __hip_atomic_store(wsq.qr + me, (unsigned long long)(unsigned)WS_SENT << 32, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
-                    wide_walk_pool(bvh, wL, (unsigned *)(smem + (size_t)112 * bvh.wnodes), wsstride, wpool, !walking,
-                                   ray, shadow, walk, split, (sflags >> 8) & 255);
-                    // (the ray comes back from the slot on every path, so
-                    // it is not held in registers across the call)
-                    const uint2 rr = wpool.res[me];
-                    const uint4 a = wpool.p0[me], b = wpool.p1[me];
-                    ray.o = mk(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z));
-                    ray.d = mk(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z));
-                    walking = (int)rr.y == POOL_SENT;
+                    const unsigned long long pm = __builtin_amdgcn_ballot_w64(!walking);
+                    if (pm) {
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        if (lane == __builtin_ctzll(__builtin_amdgcn_read_exec())) {
+                            unsigned *rw = wsq.ready + 2 * (wave - nwalk);
+                            if ((unsigned)pm)
+                                __hip_atomic_fetch_or(rw, (unsigned)pm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if ((unsigned)(pm >> 32))
+                                __hip_atomic_fetch_or(rw + 1, (unsigned)(pm >> 32), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                    }
+                    walking = true;
+                    const int nwait = __builtin_popcountll(__builtin_amdgcn_read_exec());
+                    const int want = max(1, (nwait * ((sflags >> 8) & 255) + 63) >> 6), maxpolls = (sflags >> 16) & 255;
+                    unsigned long long res;
+                    unsigned polls = 0;
+                    while (true) {
+                        res = __hip_atomic_load(wsq.qr + me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        const int nr = __builtin_popcountll(__builtin_amdgcn_ballot_w64((int)(res >> 32) != WS_SENT));
+                        if (nr >= want || (nr > 0 && polls >= (unsigned)maxpolls)) break;
+                        if (++polls > WS_SPIN_MAX ||
+                            __hip_atomic_load(wsq.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                            if (lane == __builtin_ctzll(__builtin_amdgcn_read_exec())) {
+                                __hip_atomic_store(wsq.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                atomicAdd(work + 3, 1);
+                            }
+                            res = (unsigned long long)(unsigned)-1 << 32;   // (abandoned: a miss)
+                            k = nsamples;
+                            exhausted = true;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    walking = (int)(res >> 32) == WS_SENT;
 #ifdef RT_SPT_TRACE
                     tr_walk += (unsigned)(__builtin_amdgcn_s_memtime() - tr_w0);
 #endif
                     if (walking) continue;
                     SPT_PROF(PB_WSHADE);
-                    t = __uint_as_float(rr.x);
-                    id = (int)rr.y;
+                    t = __uint_as_float((unsigned)res);
+                    id = (int)(res >> 32);
                     first = id;
                 } else {
                 if (!walking) wide_begin<COUNT>(bvh, ray, shadow, t, walk);
-                // (pooled builds: only the cooperative walk here -- the host
-                // launches them with the pool on)
                 if constexpr (CG != 0)
                     walking = coop ? !wide_walk_coop<COUNT, (CG == 4 ? 4 : 8)>(bvh, wL, wstk, ray, shadow, walk, split)
-                                   : POOLED ? false : !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
+                                   : !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
                 else
-                    walking = POOLED ? false : !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
+                    walking = !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
 #ifdef RT_SPT_TRACE
                 tr_walk += (unsigned)(__builtin_amdgcn_s_memtime() - tr_w0);
 #endif
@@ -2286,11 +1918,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 first = id;                 // any hit: the highest occluder (COUNT)
                 }
             } else {
-#if RT_SPT_QV == 2
                 id = query_bf<COUNT>(geo, ray, t, first);
-#else
-                id = query<COUNT>(geo, ray, t, first);
-#endif
             }
             float dp = 0.f, inv_sign = 1.f;  // REFR (pass A): vdot(normal, ray.d), -1 * sign(dp); and id
             if (DUAL && fin) {
@@ -2648,6 +2276,9 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         const unsigned long long c[4] = {cnt.isect, cnt.isectp, COUNT ? cnt.tests : 0ull, cnt.samples};
         flush_counters<4>(counters, c);
     }
+    if constexpr (WS) {                 // this shader wave posts nothing more
+        if (lane == 0) __hip_atomic_fetch_add(wsq.ctl, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
 #ifdef RT_SPT_PROF
 #pragma unroll
     for (int b = 0; b < PB_N; b++) {
@@ -2784,29 +2415,85 @@ struct spt_scene {
     mutable std::mutex work_mu;
     mutable int work_next = 0;
     mutable unsigned long long work_captured = 0;
-    int wide_wpb = 16;                // waves per block of the 8-wide launches (fixed at build: the LDS fit)
     bool no_refr = false;             // no sphere has refl == REFR (render_kernel sflags bit 0)
 };
 
 namespace {
 // 8-wide hierarchy launches: blocks of WIDE_WPB waves (each holds its own
 // LDS copy of the nodes and its waves' stacks), one per CU at the kernel's
-// occupancy of 4 waves per SIMD.  RT_WIDE_WPB / RT_WIDE_BLOCKS: A/B.
+// occupancy of 4 waves per SIMD.
 constexpr int WIDE_WPB = 16;
 constexpr size_t WIDE_LDS_MAX = 144 * 1024;
-int wide_wpb()
-{
-    const char *e = getenv("RT_WIDE_WPB");
-    const int v = e ? atoi(e) : WIDE_WPB;
-    return v >= 1 && v <= 16 ? v : WIDE_WPB;
-}
 size_t wide_lds_bytes(int wnodes, int wdepth, int wpb, bool counted = true)
 {
     return (size_t)(counted ? 144 : 112) * wnodes + (size_t)wpb * 256 * (wdepth > 1 ? wdepth - 1 : 1);
 }
-}  // namespace
 
-namespace {
+// The launch policy's tuning knobs, in one place.  The defaults are the
+// measured best; RT_SPT_TUNE="key=value,..." overrides any of
+// them for an A/B run or a test (read at every launch, so a test may change
+// it between frames).  Keys:
+//   coop=N      cooperative (tier-1) tiles of an ordered 8-wide launch
+//               (default: 2 x CUs at <= 5 waves of work per SIMD, 4 x CUs at
+//               <= 10, else 0)
+//   coop_g=G    lanes per pixel of those tiles, 8 or 4 (default 8 at <= 5
+//               waves per SIMD, 4 above)
+//   coop_waves=K waves of each block that fetch tier-1 sub-items first (16)
+//   routed=N    tier-2 tiles routed one per SIMD (default 4 x blocks when
+//               there is no cooperative tier, else 0)
+//   walk=B/P/S  wide_walk: trip budget per call, leaf batch threshold and
+//               early stop, both in 1/64 of the call's lanes (16/16/32)
+//   prio=A/B/C  priority-levelling boundaries in 1/256 of the samples
+//               (64/128/192 for the 4-wave block shape, 128/192/224 for 16)
+//   wpb=4|16    full-scan block shape (default: by waves of work per SIMD)
+//   blocks=N    8-wide persistent grid size (default: one block per CU)
+//   ws=0|1      split walk / shade roles for 8-wide launches without a
+//               cooperative tier (render_kernel<..., WS>)
+//   ws_walkers=K  walker waves per block (4: one per SIMD)
+//   ws_walk=B/P/S their wide_walk budget / batch / stop
+//   ws_wait=F/M a shader wave shades once F/64 of its waiting lanes have
+//               results, or after M polls with at least one
+//   ws_prio=W/S walker / shader waves' issue priority (0..3)
+struct SptTune {
+    int coop = -1, coop_g = 0, coop_waves = -1, routed = -1;
+    int budget = 16, batch = 16, stop = 32;
+    int prio[3] = {-1, -1, -1};
+    int wpb = 0, blocks = 0;
+    int ws = 0, ws_walkers = 4, ws_budget = 8, ws_batch = 16, ws_stop = 48, ws_frac = 32, ws_polls = 16;
+    int ws_prio_walk = 2, ws_prio_shade = 1;
+};
+SptTune spt_tune()
+{
+    SptTune t;
+    const char *e = getenv("RT_SPT_TUNE");
+    if (!e) return t;
+    std::string all(e);
+    size_t pos = 0;
+    while (pos < all.size()) {
+        size_t end = all.find(',', pos);
+        if (end == std::string::npos) end = all.size();
+        const std::string kv = all.substr(pos, end - pos);
+        pos = end + 1;
+        const size_t eq = kv.find('=');
+        if (eq == std::string::npos) continue;
+        const std::string k = kv.substr(0, eq);
+        const char *v = kv.c_str() + eq + 1;
+        if (k == "coop") t.coop = std::max(atoi(v), 0);
+        else if (k == "coop_g") t.coop_g = atoi(v) == 4 ? 4 : 8;
+        else if (k == "coop_waves") t.coop_waves = std::min(std::max(atoi(v), 0), 16);
+        else if (k == "routed") t.routed = std::max(atoi(v), 0);
+        else if (k == "walk") sscanf(v, "%d/%d/%d", &t.budget, &t.batch, &t.stop);
+        else if (k == "prio") sscanf(v, "%d/%d/%d", &t.prio[0], &t.prio[1], &t.prio[2]);
+        else if (k == "wpb") t.wpb = atoi(v) == 16 ? 16 : 4;
+        else if (k == "blocks") t.blocks = std::max(atoi(v), 0);
+        else if (k == "ws") t.ws = atoi(v) != 0;
+        else if (k == "ws_walkers") t.ws_walkers = std::min(std::max(atoi(v), 1), 15);
+        else if (k == "ws_walk") sscanf(v, "%d/%d/%d", &t.ws_budget, &t.ws_batch, &t.ws_stop);
+        else if (k == "ws_wait") sscanf(v, "%d/%d", &t.ws_frac, &t.ws_polls);
+        else if (k == "ws_prio") sscanf(v, "%d/%d", &t.ws_prio_walk, &t.ws_prio_shade);
+    }
+    return t;
+}
 
 // Launch shape: one wave per 8x8 tile of rows [r0, r1).  256-thread blocks
 // (several per CU, dispatched as CUs free up) unless the window has at most
@@ -2819,9 +2506,9 @@ struct Shape {
     int nslots = 0;                   // dispatch slots (tile groups of four) the order / cost arrays cover
     const int *order = nullptr;       // adaptive schedule (render_kernel's group_order / group_cost)
     unsigned *cost = nullptr;
-    int heavy16 = 0;                  // with order: heaviest slots kept at top priority, in 16s
     bool tiers = true;                // with order: its first tiles get the heavy-tile treatment
     bool cost_max = false;            // cost: a group's longest tile (atomic max), not the sum
+    SptTune tune;
 };
 // Rows [r0, r1), or (gstride > 1) the 8-row groups r0/8, r0/8 + gstride, ...
 // below r1 (r0 a multiple of 8); or (nlist > 0) the nlist tile groups of a
@@ -2829,6 +2516,7 @@ struct Shape {
 Shape launch_shape(const spt_scene &sc, int w, int r0, int r1, int gstride = 1, int nlist = 0)
 {
     Shape g;
+    g.tune = spt_tune();
     g.tiles_x = (w + 7) / 8;
     g.gstride = gstride;
     const int groups = (r1 - r0 + 7) / 8;
@@ -2842,21 +2530,14 @@ Shape launch_shape(const spt_scene &sc, int w, int r0, int r1, int gstride = 1, 
     // ms); otherwise 256-thread blocks at the kernel's occupancy.
     const double wps = (double)work / (4.0 * sc.cus);
     g.wpb = (wps <= 4.0 || (wps > 6.0 && wps <= 8.0)) ? 16 : 4;
-    if (const char *e = getenv("RT_SPT_WPB")) g.wpb = atoi(e) == 16 ? 16 : 4;   // A/B
+    if (g.tune.wpb) g.wpb = g.tune.wpb;
     g.nblocks = (work + g.wpb - 1) / g.wpb;
     g.nslots = nlist > 0 ? nlist : g.nblocks * (g.wpb / 4);
     if (sc.bvh.wnode) {               // persistent waves: one block per CU (fewer for a small window)
-        g.wpb = sc.wide_wpb;
-        g.nblocks = (work + g.wpb - 1) / g.wpb;
+        g.wpb = WIDE_WPB;
+        g.nblocks = std::min(sc.cus, (work + g.wpb - 1) / g.wpb);
+        if (g.tune.blocks) g.nblocks = g.tune.blocks;
         g.nslots = nlist > 0 ? nlist : (g.ntiles + 3) / 4;
-#if RT_WIDE_PERSIST
-        g.nblocks = std::min(sc.cus, g.nblocks);
-        if (const char *e = getenv("RT_WIDE_BLOCKS")) g.nblocks = std::max(1, atoi(e));   // A/B
-#else
-        g.wpb &= ~3;                  // static: whole groups per block, a slot per group
-        g.nblocks = (work + g.wpb - 1) / g.wpb;
-        g.nslots = nlist > 0 ? nlist : g.nblocks * (g.wpb / 4);
-#endif
     }
     return g;
 }
@@ -2865,13 +2546,12 @@ Shape launch_shape(const spt_scene &sc, int w, int r0, int r1, int gstride = 1, 
 // 1/2, 3/4 of the samples for the full-frame shape; for the 16-wave block
 // shape (multi-GPU windows of <= 8 waves per SIMD, one or two rounds) at
 // 1/2, 3/4, 7/8 -- finer where the co-resident waves drain.
-// RT_SPT_PRIO_SCHED=a,b,c (in 1/256) overrides it (A/B).
 int prio_schedule(const Shape &g)
 {
     int a = 64, b = 128, c = 192;
     if (g.wpb == 16) { a = 128; b = 192; c = 224; }
-    if (const char *e = getenv("RT_SPT_PRIO_SCHED")) sscanf(e, "%d,%d,%d", &a, &b, &c);
-    return (a & 255) | ((b & 255) << 8) | ((c & 255) << 16) | ((g.order ? g.heavy16 & 255 : 0) << 24);
+    if (g.tune.prio[0] >= 0) { a = g.tune.prio[0]; b = g.tune.prio[1]; c = g.tune.prio[2]; }
+    return (a & 255) | ((b & 255) << 8) | ((c & 255) << 16);
 }
 
 // A zeroed work-counter quad of the scene's ring for one persistent launch
@@ -2902,24 +2582,13 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
     const int n = sc.n;
     const float4 *gg = sc.d_soa, *ge = gg + n, *gc = ge + n, *gl = gc + n;
     size_t lds = LDS ? (size_t)(3 * n + 3 * std::max(sc.nlights, 1)) * sizeof(float4) : 0;
-    if (GEO == rt::smallpt::GEO_BVH && RT_SPT_GSTORE) lds = (size_t)(g.wpb / 4) * rt::smallpt::GS_BYTES;
+    if (GEO == rt::smallpt::GEO_BVH) lds = (size_t)(g.wpb / 4) * rt::smallpt::GS_BYTES;
     if (g.wpb == 16 && lds < 81 * 1024) lds = 81 * 1024;   // > half the CU's 160 KiB: one block per CU
     int *work = nullptr;
-    int sflags = (sc.no_refr && !getenv("RT_SPT_FULL_PASSA")) ? 1 : 0;   // (env: A/B)
+    int sflags = sc.no_refr ? 1 : 0;
     if (g.cost_max) sflags |= 4;
     if (GEO == rt::smallpt::GEO_WIDE) {
         lds = wide_lds_bytes(sc.bvh.wnodes, sc.bvh.wdepth, g.wpb, COUNT);
-        // The block pool of parked walks (RT_WIDE_POOL builds, uncounted
-        // kernels) when it fits beside the nodes and stacks; RT_SPT_POOL=0
-        // turns it off, RT_SPT_POOL=k sets the claim threshold (k/64 idle).
-        if (RT_WIDE_POOL && !COUNT && lds + rt::smallpt::pool_bytes() <= 160 * 1024) {
-            const char *e = getenv("RT_SPT_POOL");
-            const int refill = e ? atoi(e) : RT_WIDE_POOL_REFILL;
-            if (refill > 0) {
-                lds += rt::smallpt::pool_bytes();
-                sflags |= 2 | (std::min(refill, 65) << 8);
-            }
-        }
         if (!(work = work_entry(sc, s))) return rtrt::check_launch("spt work counters") ? RT_ERR_HIP : RT_ERR_INVALID;
     }
     // Heavy tiles (with a learnt order, GEO_WIDE persistent launches), in
@@ -2932,11 +2601,12 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
     // which the cooperative walk shortens ~2x at ~3x their issue cost.
     // configs[4], 64 spp (profiles/r03/c4_coop_*.log): N = 8 windows
     // 18.0-19.8 -> 11.4-15.1 ms, N = 4 18.7 -> 17 ms; see DESIGN.md.
+    const SptTune &tu = g.tune;
     int n1 = 0, n2 = 0, sp = 0, kcg = 0;
-    if (GEO == rt::smallpt::GEO_WIDE && RT_WIDE_PERSIST && g.order && g.tiers) {
+    if (GEO == rt::smallpt::GEO_WIDE && g.order && g.tiers) {
         n2 = std::min(4 * g.nblocks, 4 * g.nslots);
         const double wps = (double)g.work / (4.0 * sc.cus);
-        int hw = 0, cg = RT_SPT_COOP_G;
+        int hw = 0, cg = 8;
         if (wps <= 5.0) {
             n1 = 2 * sc.cus;
             hw = 16;
@@ -2951,40 +2621,48 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
             hw = 16;
             cg = 4;
         }
-        if (const char *e = getenv("RT_WIDE_COOP_G")) cg = atoi(e) == 4 ? 4 : 8;              // A/B
-        if (const char *e = getenv("RT_WIDE_COOP")) n1 = std::max(atoi(e), 0);                  // A/B
-        if (const char *e = getenv("RT_WIDE_HEAVY_WAVES")) hw = std::min(std::max(atoi(e), 0), 16);   // A/B
+        if (tu.coop_g) cg = tu.coop_g;
+        if (tu.coop >= 0) n1 = tu.coop;
+        if (tu.coop_waves >= 0) hw = tu.coop_waves;
         if (n1 > 0) n2 = 0;   // routed tiles beside cooperative ones: N = 4 17 -> 24 ms (c4_coop_tiers_ab.log)
-        if (const char *e = getenv("RT_WIDE_HEAVY")) n2 = std::max(atoi(e), 0);                 // A/B
+        if (tu.routed >= 0) n2 = tu.routed;
         n1 = std::min(n1, 4 * g.nslots);
         n2 = std::min(n2, 4 * g.nslots - n1);
         if (n1 > 0) sp = (cg == 8 ? 3 : 2) | 4 | (hw << 3);
         kcg = n1 > 0 ? cg : 0;
-        if (const char *e = getenv("RT_SPT_SPLIT")) {   // A/B: tier 1 split 2^k ways, a lane per pixel (k < 3)
-            const int k = std::min(std::max(atoi(e), 0), 3);
-            sp = (k == 3 ? (cg == 8 ? 3 : 2) | 4 : k) | (hw << 3);
-            kcg = k == 3 && n1 > 0 ? cg : 0;
-        }
     }
     const int nheavy = std::min(n1, 0xffff) | (std::min(n2, 0xffff) << 16);
     int split = 0;
     if (GEO == rt::smallpt::GEO_WIDE) {
-        int budget = RT_WIDE_BUDGET, batch = RT_BVH_BATCH, stop = RT_WIDE_STOP;
-        if (const char *e = getenv("RT_WIDE_OPTS")) sscanf(e, "%d,%d,%d", &budget, &batch, &stop);   // tools: A/B
-        split = (RT_WIDE_PERSIST ? sp : 0) | (std::min(std::max(budget, 1), 255) << 8) |
-                (std::min(std::max(batch, 0), 64) << 16) | (std::min(std::max(stop, 0), 64) << 24);
+        split = sp | (std::min(std::max(tu.budget, 1), 255) << 8) | (std::min(std::max(tu.batch, 0), 64) << 16) |
+                (std::min(std::max(tu.stop, 0), 64) << 24);
     }
     // (the kernel carries the cooperative walk only when this launch has a
     // cooperative tier, and only the group size it uses)
     auto kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 0>;
+    int wsopt = 0;
     if constexpr (GEO == rt::smallpt::GEO_WIDE) {
         if (kcg == 8) kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 8>;
         else if (kcg == 4) kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 4>;
+        // Split walk / shade roles where every tile runs a lane per pixel
+        // (uncounted or rays-only launches without a cooperative tier).
+        const int nwalk = std::min(tu.ws_walkers, g.wpb - 1);
+        const size_t ws_lds = lds + rt::smallpt::ws_bytes((g.wpb - nwalk) * 64);
+        if constexpr (!COUNT) {
+            if (tu.ws && kcg == 0 && ws_lds <= 160 * 1024) {
+                kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 0, true>;
+                lds = ws_lds;
+                wsopt = nwalk | ((tu.ws_prio_walk & 3) << 4) | (std::min(std::max(tu.ws_budget, 1), 255) << 8) |
+                        (std::min(std::max(tu.ws_batch, 0), 64) << 16) | (std::min(std::max(tu.ws_stop, 0), 64) << 24);
+                sflags |= (std::min(std::max(tu.ws_frac, 0), 64) << 8) | (std::min(std::max(tu.ws_polls, 0), 255) << 16) |
+                          ((tu.ws_prio_shade & 3) << 24);
+            }
+        }
     }
     hipLaunchKernelGGL(kern, dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.nslots, g.gstride, first,
                        ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt, work, split,
-                       nheavy, sflags);
+                       nheavy, sflags, wsopt);
     return RT_OK;
 }
 
@@ -3058,13 +2736,10 @@ int build_scene_bvh(spt_scene *sc, const rt_sphere *spheres)
     bool wide = false;
     const char *we = getenv("RT_SPT_WIDE");             // 0: the binary walk only (A/B, tests)
     if (nn && !(we && atoi(we) == 0)) {
-        int first = 8;                                  // RT_SPT_WIDE_LEAF: A/B of the leaf size
-        if (const char *e = getenv("RT_SPT_WIDE_LEAF")) first = std::min(std::max(atoi(e), 1), 16);
-        sc->wide_wpb = wide_wpb();                      // (RT_WIDE_WPB: A/B) read once, here
-        for (int lm : {first, 8, 12, 16}) {
+        for (int lm : {8, 12, 16}) {    // (leaves of <= 5 or 6: slower, profiles/r03/c4_leaf_size_ab.log)
             wb.leaf_max = lm;
             wb.build(b);
-            if (wide_lds_bytes(wb.nnodes, wb.depth, sc->wide_wpb) <= WIDE_LDS_MAX) { wide = true; break; }
+            if (wide_lds_bytes(wb.nnodes, wb.depth, WIDE_WPB) <= WIDE_LDS_MAX) { wide = true; break; }
         }
     }
     std::vector<float4> geo(nb + na);
@@ -3286,16 +2961,6 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
     }
     if (q.state == 2) {
         g.order = q.d_order;
-        // Heaviest groups kept at the top issue priority throughout: none
-        // since round 5 (configs[4], same box: cus/4 groups 24.7-26.3 ms, 16
-        // 24.5-25.6, 0 24.2 ms; N = 8 windows 0/8 11.2 -> 10.2, 3/8 12.2 ->
-        // 11.0 ms; N = 4, 2 level -- profiles/r05/c4_heavy_prio_sweep.log):
-        // every wave levels its priority down by progress, and a wave held
-        // at the top starves its SIMD's others.  (Round 2, binary walk:
-        // cus/4 was best.)  RT_SPT_HEAVY=n: A/B.
-        int heavy = 0;
-        if (const char *he = getenv("RT_SPT_HEAVY")) heavy = atoi(he);
-        g.heavy16 = std::min(std::max((heavy + 15) / 16, 0), 255);
         return false;
     }
     if (q.state == 0) {
@@ -3306,9 +2971,7 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
         // routed tiles) goes to the first groups in order, and a group with
         // one very long tile outranks four middling ones (configs[4] N = 4
         // interleaved windows 17.1 -> 16.3 ms; the full frame level).
-        // RT_SPT_COST_MAX=0: the sum (A/B).
-        const char *cm = getenv("RT_SPT_COST_MAX");
-        g.cost_max = !(cm && atoi(cm) == 0);
+        g.cost_max = true;
         return true;
     }
     return false;                                       // state 1, read-back in flight: plain launch
@@ -3336,7 +2999,7 @@ int scene_render(const spt_scene *sc, const rt_camera *camera, float *d_colors, 
     bool record = false;
     if (d_list) {
         // The caller's order, heaviest first: its first groups get the
-        // heavy-tile treatment (top priority, cooperative or routed tiles)
+        // heavy-tile treatment (cooperative or routed tiles)
         // as with a learnt order -- unless the launch records costs
         // (d_cost): the list is then taken as unordered and every tile runs
         // a lane per pixel, so the recorded costs compare like with like.
@@ -3344,9 +3007,6 @@ int scene_render(const spt_scene *sc, const rt_camera *camera, float *d_colors, 
         grid.cost = sc->bvh.node ? d_cost : nullptr;
         grid.cost_max = (mode & SPT_COST_MAX) != 0;
         grid.tiers = d_cost == nullptr;
-        grid.heavy16 = 0;                 // (no group held at the top priority: see sched_before)
-        if (const char *he = getenv("RT_SPT_HEAVY"))
-            if (!d_cost) grid.heavy16 = std::min(std::max((atoi(he) + 15) / 16, 0), 255);
     } else {
         record = sched_before(*sc, grid, s, w, h, row_begin, row_end, gstride, nsamples, base, *camera,
                               d_counters && !(mode & SPT_COUNT_RAYS));
@@ -3503,7 +3163,7 @@ namespace rtrt {
 std::string scene_prep_hooks()
 {
     std::string h;
-    for (const char *k : {"RT_SPT_NO_BVH", "RT_SPT_GEO", "RT_SPT_WIDE", "RT_SPT_WIDE_LEAF", "RT_WIDE_WPB"}) {
+    for (const char *k : {"RT_SPT_NO_BVH", "RT_SPT_GEO", "RT_SPT_WIDE"}) {
         const char *v = getenv(k);
         h += v ? v : "-";
         h += "|";
@@ -3613,17 +3273,6 @@ extern "C" int spt_prof_read(unsigned long long *out)
     static const unsigned long long zero[2 * rt::smallpt::PB_N] = {};
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(rt::smallpt::g_spt_prof), zero, sizeof(zero));
     return e == hipSuccess ? RT_OK : rtrt::fail_hip(e, "spt_prof_read");
-}
-#endif
-
-#ifdef RT_BVH_STATS
-// Tools-only: reads and clears the traversal statistics (16 counters).
-extern "C" int spt_bvh_stats_read(unsigned long long *out)
-{
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(rt::smallpt::g_bvh_stats), sizeof(rt::smallpt::g_bvh_stats));
-    static const unsigned long long zero[24] = {};
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(rt::smallpt::g_bvh_stats), zero, sizeof(zero));
-    return e == hipSuccess ? RT_OK : rtrt::fail_hip(e, "spt_bvh_stats_read");
 }
 #endif
 

@@ -192,7 +192,7 @@ def test_configs4_cooperative_walk_golden(rt, oracle, counted, coop, monkeypatch
     uncounted."""
     import json
     import os
-    monkeypatch.setenv("RT_WIDE_COOP", coop)
+    monkeypatch.setenv("RT_SPT_TUNE", "coop=" + coop)
     gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
     g = gold["smallpt"]["1920x1080_64spp_complex10k"]
     spheres, n, cam = rt.scenes.complex10k()

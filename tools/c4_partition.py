@@ -124,14 +124,13 @@ def main():
         print("  learnt costs: total %d ticks, max group %d, predicted per-rank loads %s" % (
             c.sum(), c.max(), [int(c[p].sum()) for p in parts]), flush=True)
         # SWEEP="n1:hw,..." times the balanced lists under other heavy-tile
-        # policies (RT_WIDE_COOP = cooperative tiles, RT_WIDE_HEAVY_WAVES =
-        # waves per block that fetch them first); "-" = the library default.
+        # policies (RT_SPT_TUNE coop = cooperative tiles, coop_waves = waves
+        # per block that fetch them first); "-" = the library default.
+        tune0 = os.environ.get("RT_SPT_TUNE")
         for pol in os.environ.get("SWEEP", "-").split(","):
-            for key in ("RT_WIDE_COOP", "RT_WIDE_HEAVY_WAVES"):
-                os.environ.pop(key, None)
             if pol != "-":
                 n1, hw = pol.split(":")
-                os.environ["RT_WIDE_COOP"], os.environ["RT_WIDE_HEAVY_WAVES"] = n1, hw
+                os.environ["RT_SPT_TUNE"] = "coop=%s,coop_waves=%s" % (n1, hw) + ("," + tune0 if tune0 else "")
             out = bufs()
             res = []
             for k in range(N):
@@ -144,8 +143,10 @@ def main():
             ok = torch.equal(out[0].view(torch.int32), ref[0].view(torch.int32)) and torch.equal(out[2], ref[2]) \
                 and torch.equal(out[1], ref[1])
             print("  assembled == full frame: %s" % ok, flush=True)
-        for key in ("RT_WIDE_COOP", "RT_WIDE_HEAVY_WAVES"):
-            os.environ.pop(key, None)
+        if tune0 is None:
+            os.environ.pop("RT_SPT_TUNE", None)
+        else:
+            os.environ["RT_SPT_TUNE"] = tune0
         sc.close()
 
 
