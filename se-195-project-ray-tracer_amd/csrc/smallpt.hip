@@ -1184,174 +1184,6 @@ __device__ uint4 *g_spt_trace;
 __device__ int g_spt_only_group = -1;
 #endif
 
-// ---------------------------------------------------------------------------
-// Split walk / shade (WS): the 8-wide kernels with warp-specialised waves.
-//
-// In the one-role kernel every lane owns one pixel and walks its own queries:
-// configs[4]'s node steps ran with 31.5 of 64 lanes and its leaf passes with
-// 18.9 (profiles/r05), because a wave's lanes need different numbers of
-// trips, and a walk can only be continued by the lane that owns its pixel's
-// path state.  Here the block's waves take one of two roles:
-//   * shader waves (waves nwalk..15) each hold a pixel per lane -- its RNG
-//     words, accumulator and path state in VGPRs, as render_kernel's loop --
-//     and, where that loop walks, post the query into the lane's LDS slot
-//     and wait for its result;
-//   * walker waves (waves 0..nwalk-1, one per SIMD at nwalk = 4) claim posted
-//     queries, walk them (wide_walk: the same trips, the same float
-//     operations), write each result into its slot and claim the next query
-//     as soon as a lane is free.
-// With 12 shader waves there are 768 queries in flight per CU for 256 walker
-// lanes, so a walker lane that finishes finds another query waiting: node
-// steps and leaf passes run with (nearly) full waves however the trip
-// counts differ.  Results are the reference's: a query's result (nearest
-// distance, highest index on ties; or "some occluder") does not depend on
-// which lane walks it, and each pixel still runs its own samples, draws and
-// float operations in order -- only the lane that tests its spheres changes.
-//
-// LDS after the nodes and stacks (ws_bytes): per shader slot the query
-// (origin + t on entry, direction + shadow flag: 32 B) and its result (t, id:
-// 8 B; id = WS_SENT while pending), then one ready bit per slot (posted, not
-// yet claimed: 2 words per shader wave) and a control word (shader waves
-// still running).  Hand-offs are LDS-only: plain stores, a workgroup-scope
-// release, a bit set by atomic OR; claims by atomic AND, a workgroup-scope
-// acquire; results by one 64-bit store the owner polls.
-constexpr int WS_SENT = (int)0x80000000;
-__host__ __device__ constexpr size_t ws_bytes(int nslots) { return (size_t)nslots * 40 + (size_t)(nslots / 32) * 4 + 16; }
-struct WsLds {
-    float4 *qo, *qd;        // per slot: origin.xyz, t on entry | direction.xyz, shadow (0 / 1)
-    unsigned long long *qr; // per slot: result t bits | id << 32 (id = WS_SENT: pending)
-    unsigned *ready;        // nslots / 32 words
-    int *ctl;               // [0]: shader waves still running, [1]: abort (a spin ran past its bound)
-};
-__device__ __forceinline__ WsLds ws_carve(char *base, int nslots)
-{
-    WsLds Q;
-    Q.qo = (float4 *)base;
-    Q.qd = Q.qo + nslots;
-    Q.qr = (unsigned long long *)(Q.qd + nslots);
-    Q.ready = (unsigned *)(Q.qr + nslots);
-    Q.ctl = (int *)(Q.ready + nslots / 32);
-    return Q;
-}
-// Position of the r-th (from 0) set bit of v (r < popcount(v)).
-__device__ __forceinline__ int nth_set_bit(unsigned v, int r)
-{
-    int pos = 0;
-#pragma unroll
-    for (int sz = 16; sz >= 1; sz >>= 1) {
-        const unsigned lo = v & ((1u << sz) - 1u);
-        const int c = __builtin_popcount(lo);
-        if (r >= c) {
-            r -= c;
-            v >>= sz;
-            pos += sz;
-        } else {
-            v = lo;
-        }
-    }
-    return pos;
-}
-// Spin bound of every WS wait (s_sleep 1 per poll: ~seconds): past it the
-// block aborts -- a wrong frame and a flagged error (counters[... ] is not
-// touched; the host sees it through ws_abort) instead of a hung GPU.
-constexpr unsigned WS_SPIN_MAX = 1u << 24;
-
-// s_setprio with a run-time level (the instruction takes an immediate).
-__device__ __forceinline__ void set_prio(int p)
-{
-    if (p == 3) __builtin_amdgcn_s_setprio(3);
-    else if (p == 2) __builtin_amdgcn_s_setprio(2);
-    else if (p == 1) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-}
-
-// The walker role.  opts: wide_walk's budget / batch / stop (bits 8..31 as
-// render_kernel's split); nwords: ready words (shader slots / 32).
-__device__ void ws_walker(const BvhView &B, const uint4 *__restrict__ L, unsigned *__restrict__ stk, const WsLds &Q,
-                          int nwords, int opts, int *abort_flag)
-{
-    const int lane = threadIdx.x & 63;
-    int slot = -1;
-    ray3 r;
-    bool shadow = false;
-    BvhWalk W;
-#ifdef RT_SPT_PROF
-    for (int b = 0; b < 3; b++) W.pf_l[b] = W.pf_w[b] = 0;
-#endif
-#ifdef RT_SPT_TRACE
-    W.tr_leaf = W.tr_trips = W.tr_leafruns = 0;
-#endif
-    int scan = (int)(threadIdx.x >> 6) * 5 % nwords;   // (walker waves start their claims on different words)
-    unsigned spins = 0;
-    while (true) {
-        // ---- idle lanes claim posted queries: one ready word per round, up
-        // to two rounds (its lanes rank themselves among the idle ones)
-#pragma unroll 1
-        for (int round = 0; round < 2; round++) {
-            const unsigned long long im = __builtin_amdgcn_ballot_w64(slot < 0);
-            if (!im) break;
-            const unsigned v = lane < nwords ? __hip_atomic_load(Q.ready + lane, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
-            const unsigned long long nz = __builtin_amdgcn_ballot_w64(v != 0u);
-            if (!nz) break;
-            // the first non-empty word at or after `scan`
-            const unsigned long long rot = (nz >> scan) | (scan ? nz << (64 - scan) : 0ull);
-            const int wd = (__builtin_ctzll(rot) + scan) % 64;
-            scan = (wd + 1) % nwords;
-            const unsigned cw = __builtin_amdgcn_readlane(v, wd);
-            const int want = __builtin_popcountll(im);
-            const unsigned take = __builtin_popcount(cw) <= want ? cw : cw & ((1u << nth_set_bit(cw, want)) - 1u);
-            unsigned got = 0;
-            if (lane == __builtin_ctzll(__builtin_amdgcn_read_exec()))
-                got = __hip_atomic_fetch_and(Q.ready + wd, ~take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & take;
-            got = __builtin_amdgcn_readfirstlane(got);
-            if (!got) continue;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
-            if (slot < 0 && rank < __builtin_popcount(got)) {
-                slot = 32 * wd + nth_set_bit(got, rank);
-                const float4 a = Q.qo[slot], b = Q.qd[slot];
-                r.o = mk(a.x, a.y, a.z);
-                r.d = mk(b.x, b.y, b.z);
-                shadow = __float_as_int(b.w) != 0;
-                wide_begin<false>(B, r, shadow, a.w, W);
-            }
-        }
-        const unsigned long long bm = __builtin_amdgcn_ballot_w64(slot >= 0);
-        if (!bm) {
-            if (__hip_atomic_load(Q.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) break;
-            if (++spins > WS_SPIN_MAX || __hip_atomic_load(Q.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                if (lane == 0) {
-                    __hip_atomic_store(Q.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    atomicAdd(abort_flag, 1);
-                }
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        spins = 0;
-        if (slot >= 0) {
-            const bool done = wide_walk<false>(B, L, stk, r, shadow, W, opts);
-            if (done) {
-                const unsigned long long res = (unsigned long long)__float_as_uint(W.t) |
-                                               ((unsigned long long)(unsigned)W.id << 32);
-                __hip_atomic_store(Q.qr + slot, res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                slot = -1;
-            }
-        }
-    }
-#ifdef RT_SPT_PROF
-    for (int b = 0; b < 3; b++) {   // walker lanes / wave-executions of calls, node steps, leaf passes
-        const unsigned long long l = wave_sum_u64(W.pf_l[b]), v = wave_sum_u64(W.pf_w[b]);
-        if (lane == 0) {
-            atomicAdd(&g_spt_prof[2 * (PB_WCALL + b)], l);
-            atomicAdd(&g_spt_prof[2 * (PB_WCALL + b) + 1], v);
-        }
-    }
-#endif
-}
-
 // toInt, vec.h:62 (clamp macro keeps -0.0; glibc powf via rt_glibc_math.h).
 __device__ __forceinline__ int to_int(float x)
 {
@@ -1386,13 +1218,7 @@ constexpr int GS_BYTES = 6160;      // GEO_BVH group staging strip: 8 x 96 colou
 // CG (8-wide kernels): lanes per pixel of the cooperative walk this kernel
 // carries (8 or 4), or 0 -- no cooperative code (windows without a
 // cooperative tier: the full frame, N = 2 shares).
-// WS (8-wide, uncounted or rays-only, CG = 0): split walk / shade roles
-// (ws_walker above); wsopt bits 0..3 = walker waves, 4..5 = their issue
-// priority, 8..31 = their wide_walk options (as split); sflags bits 8..15 =
-// the share of a shader wave's waiting lanes (in 1/64) whose results it
-// waits for before it shades, 16..23 = the most polls it waits for them,
-// 24..25 = the shader waves' issue priority.
-template <bool DL, bool COUNT, int GEO, bool DUAL = false, bool RAYS = false, int CG = 0, bool WS = false>
+template <bool DL, bool COUNT, int GEO, bool DUAL = false, bool RAYS = false, int CG = 0>
 __global__ void __launch_bounds__(1024, GEO == 2 ? ((COUNT || RAYS) ? BVH_MINWAVES_COUNT : BVH_MINWAVES)
                                               : GEO == 3 ? ((COUNT || RAYS) ? BVH_MINWAVES_COUNT : WIDE_MINWAVES)
                                               : ((DUAL && !COUNT && !RAYS) ? SPT_DUAL_MINWAVES : SPT_MINWAVES))
@@ -1404,7 +1230,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
               const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
               const float4 *__restrict__ g_col, const float4 *__restrict__ g_lrec, int nlights,
               BvhView bvh, unsigned long long *__restrict__ counters, int *__restrict__ work, int split,
-              int nheavy, int sflags, int wsopt)
+              int nheavy, int sflags)
 {
     constexpr bool LDS = GEO == GEO_LDS;
     // GEO_WIDE: persistent waves -- each wave takes 8x8 tiles from a work
@@ -1439,27 +1265,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             for (int i = threadIdx.x; i < 2 * bvh.wnodes; i += blockDim.x) d[7 * bvh.wnodes + i] = bvh.wmax[i];
         wstk = (unsigned *)(smem + (size_t)(COUNT ? 144 : 112) * bvh.wnodes) +
                (size_t)(threadIdx.x >> 6) * 64 * (bvh.wdepth - 1);
-    }
-    // WS: the query slots after every wave's stack, ready words and control
-    // zeroed (ctl[0] = the shader waves) before the barrier.
-    const int nwalk = WS ? (wsopt & 15) : 0;
-    WsLds wsq = {};
-    if constexpr (WS) {
-        const int nslot = ((int)(blockDim.x >> 6) - nwalk) * 64;
-        wsq = ws_carve(smem + (size_t)112 * bvh.wnodes + (size_t)(blockDim.x >> 6) * 256 * (bvh.wdepth - 1), nslot);
-        for (int i = threadIdx.x; i < nslot / 32; i += blockDim.x) wsq.ready[i] = 0u;
-        if (threadIdx.x == 0) {
-            wsq.ctl[0] = (int)(blockDim.x >> 6) - nwalk;
-            wsq.ctl[1] = 0;
-        }
-    }
-    if (GEO == GEO_WIDE) __syncthreads();
-    if constexpr (WS) {
-        if ((int)(threadIdx.x >> 6) < nwalk) {            // the walker role, for the whole launch
-            set_prio((wsopt >> 4) & 3);
-            ws_walker(bvh, wL, wstk, wsq, ((int)(blockDim.x >> 6) - nwalk) * 2, wsopt & ~255, work + 3);
-            return;
-        }
+        __syncthreads();
     }
 
     // 8x8 pixel tiles of the row window, one per wave, in groups of four
@@ -1582,8 +1388,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // dominates -- 28 of 64 lanes per iteration without refill, 52 with,
     // profiles/r05/c4_counted_refill.log; on the uncounted frame refill
     // measured +7 % (its waves lose the levelled priority).
-    // (WS: the shader waves always refill -- a lane's pixel is its unit)
-    const bool refill = (COUNT || WS) && PERSIST && !heavy_;
+    const bool refill = COUNT && PERSIST && !heavy_;
 #ifdef RT_SPT_TRACE
     bool active = gvalid && tile < ntiles && x < w && y < row_end &&
                   (g_spt_only_group < 0 || grp == g_spt_only_group);
@@ -1666,8 +1471,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         // round-2 rule, measured best for the binary walk, cost configs[4]
         // 2-8 % with the 8-wide one, profiles/r05/c4_heavy_prio_sweep.log).
         int prio_level = 0, prio_next = (nsamples * (prio_sched & 255)) >> 8;
-        if (WS) set_prio((sflags >> 24) & 3);
-        else __builtin_amdgcn_s_setprio(3);
+        __builtin_amdgcn_s_setprio(3);
         while (true) {
             if (refill) {
                 // ---- refill: lanes whose pixel is done store it, then take
@@ -1847,61 +1651,6 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 const unsigned long long tr_w0 = __builtin_amdgcn_s_memtime();
                 tr_queries += !walking;
 #endif
-                if constexpr (WS) {
-                    // Post the query into this lane's slot (unless it is
-                    // waiting for one already), then wait -- asleep -- until
-                    // enough of the wave's waiting lanes have their results.
-                    const int me = (wave - nwalk) * 64 + lane;
-                    if (!walking) {
-                        wsq.qo[me] = make_float4(ray.o.x, ray.o.y, ray.o.z, t);
-                        wsq.qd[me] = make_float4(ray.d.x, ray.d.y, ray.d.z, __int_as_float(shadow ? 1 : 0));
-                        __hip_atomic_store(wsq.qr + me, (unsigned long long)(unsigned)WS_SENT << 32, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                    const unsigned long long pm = __builtin_amdgcn_ballot_w64(!walking);
-                    if (pm) {
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                        if (lane == __builtin_ctzll(__builtin_amdgcn_read_exec())) {
-                            unsigned *rw = wsq.ready + 2 * (wave - nwalk);
-                            if ((unsigned)pm)
-                                __hip_atomic_fetch_or(rw, (unsigned)pm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            if ((unsigned)(pm >> 32))
-                                __hip_atomic_fetch_or(rw + 1, (unsigned)(pm >> 32), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
-                    }
-                    walking = true;
-                    const int nwait = __builtin_popcountll(__builtin_amdgcn_read_exec());
-                    const int want = max(1, (nwait * ((sflags >> 8) & 255) + 63) >> 6), maxpolls = (sflags >> 16) & 255;
-                    unsigned long long res;
-                    unsigned polls = 0;
-                    while (true) {
-                        res = __hip_atomic_load(wsq.qr + me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        const int nr = __builtin_popcountll(__builtin_amdgcn_ballot_w64((int)(res >> 32) != WS_SENT));
-                        if (nr >= want || (nr > 0 && polls >= (unsigned)maxpolls)) break;
-                        if (++polls > WS_SPIN_MAX ||
-                            __hip_atomic_load(wsq.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                            if (lane == __builtin_ctzll(__builtin_amdgcn_read_exec())) {
-                                __hip_atomic_store(wsq.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                atomicAdd(work + 3, 1);
-                            }
-                            res = (unsigned long long)(unsigned)-1 << 32;   // (abandoned: a miss)
-                            k = nsamples;
-                            exhausted = true;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                    walking = (int)(res >> 32) == WS_SENT;
-#ifdef RT_SPT_TRACE
-                    tr_walk += (unsigned)(__builtin_amdgcn_s_memtime() - tr_w0);
-#endif
-                    if (walking) continue;
-                    SPT_PROF(PB_WSHADE);
-                    t = __uint_as_float((unsigned)res);
-                    id = (int)(res >> 32);
-                    first = id;
-                } else {
                 if (!walking) wide_begin<COUNT>(bvh, ray, shadow, t, walk);
                 if constexpr (CG != 0)
                     walking = coop ? !wide_walk_coop<COUNT, (CG == 4 ? 4 : 8)>(bvh, wL, wstk, ray, shadow, walk, split)
@@ -1916,7 +1665,6 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
                 t = walk.t;
                 id = walk.id;
                 first = id;                 // any hit: the highest occluder (COUNT)
-                }
             } else {
                 id = query_bf<COUNT>(geo, ray, t, first);
             }
@@ -2276,9 +2024,6 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         const unsigned long long c[4] = {cnt.isect, cnt.isectp, COUNT ? cnt.tests : 0ull, cnt.samples};
         flush_counters<4>(counters, c);
     }
-    if constexpr (WS) {                 // this shader wave posts nothing more
-        if (lane == 0) __hip_atomic_fetch_add(wsq.ctl, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
 #ifdef RT_SPT_PROF
 #pragma unroll
     for (int b = 0; b < PB_N; b++) {
@@ -2447,20 +2192,11 @@ size_t wide_lds_bytes(int wnodes, int wdepth, int wpb, bool counted = true)
 //               (64/128/192 for the 4-wave block shape, 128/192/224 for 16)
 //   wpb=4|16    full-scan block shape (default: by waves of work per SIMD)
 //   blocks=N    8-wide persistent grid size (default: one block per CU)
-//   ws=0|1      split walk / shade roles for 8-wide launches without a
-//               cooperative tier (render_kernel<..., WS>)
-//   ws_walkers=K  walker waves per block (4: one per SIMD)
-//   ws_walk=B/P/S their wide_walk budget / batch / stop
-//   ws_wait=F/M a shader wave shades once F/64 of its waiting lanes have
-//               results, or after M polls with at least one
-//   ws_prio=W/S walker / shader waves' issue priority (0..3)
 struct SptTune {
     int coop = -1, coop_g = 0, coop_waves = -1, routed = -1;
     int budget = 16, batch = 16, stop = 32;
     int prio[3] = {-1, -1, -1};
     int wpb = 0, blocks = 0;
-    int ws = 0, ws_walkers = 4, ws_budget = 8, ws_batch = 16, ws_stop = 48, ws_frac = 32, ws_polls = 16;
-    int ws_prio_walk = 2, ws_prio_shade = 1;
 };
 SptTune spt_tune()
 {
@@ -2486,11 +2222,6 @@ SptTune spt_tune()
         else if (k == "prio") sscanf(v, "%d/%d/%d", &t.prio[0], &t.prio[1], &t.prio[2]);
         else if (k == "wpb") t.wpb = atoi(v) == 16 ? 16 : 4;
         else if (k == "blocks") t.blocks = std::max(atoi(v), 0);
-        else if (k == "ws") t.ws = atoi(v) != 0;
-        else if (k == "ws_walkers") t.ws_walkers = std::min(std::max(atoi(v), 1), 15);
-        else if (k == "ws_walk") sscanf(v, "%d/%d/%d", &t.ws_budget, &t.ws_batch, &t.ws_stop);
-        else if (k == "ws_wait") sscanf(v, "%d/%d", &t.ws_frac, &t.ws_polls);
-        else if (k == "ws_prio") sscanf(v, "%d/%d", &t.ws_prio_walk, &t.ws_prio_shade);
     }
     return t;
 }
@@ -2640,29 +2371,14 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
     // (the kernel carries the cooperative walk only when this launch has a
     // cooperative tier, and only the group size it uses)
     auto kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 0>;
-    int wsopt = 0;
     if constexpr (GEO == rt::smallpt::GEO_WIDE) {
         if (kcg == 8) kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 8>;
         else if (kcg == 4) kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 4>;
-        // Split walk / shade roles where every tile runs a lane per pixel
-        // (uncounted or rays-only launches without a cooperative tier).
-        const int nwalk = std::min(tu.ws_walkers, g.wpb - 1);
-        const size_t ws_lds = lds + rt::smallpt::ws_bytes((g.wpb - nwalk) * 64);
-        if constexpr (!COUNT) {
-            if (tu.ws && kcg == 0 && ws_lds <= 160 * 1024) {
-                kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 0, true>;
-                lds = ws_lds;
-                wsopt = nwalk | ((tu.ws_prio_walk & 3) << 4) | (std::min(std::max(tu.ws_budget, 1), 255) << 8) |
-                        (std::min(std::max(tu.ws_batch, 0), 64) << 16) | (std::min(std::max(tu.ws_stop, 0), 64) << 24);
-                sflags |= (std::min(std::max(tu.ws_frac, 0), 64) << 8) | (std::min(std::max(tu.ws_polls, 0), 255) << 16) |
-                          ((tu.ws_prio_shade & 3) << 24);
-            }
-        }
     }
     hipLaunchKernelGGL(kern, dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.nslots, g.gstride, first,
                        ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt, work, split,
-                       nheavy, sflags, wsopt);
+                       nheavy, sflags);
     return RT_OK;
 }
 

@@ -84,30 +84,9 @@ __device__ __forceinline__ float sphere_cand(float4 g, const ray3 &r, int &res)
     return cand;
 }
 
-#ifndef RT_SPHERE_EXIT
-#define RT_SPHERE_EXIT 0      // occluder spheres: all-occluded exit after each sphere some lane may hit (A/B: 1; off measured faster)
-#endif
-#ifndef RT_PLANE_ONECHECK
-#define RT_PLANE_ONECHECK 1   // occluder planes: one all-occluded check before the loop, not per plane (A/B: 0)
-#endif
-#ifndef RT_WH_LEAN
-#define RT_WH_LEAN 3        // trace()'s loops without per-lane branches: bit 0 spheres, bit 1 planes (A/B: 0)
-#endif
-
-// Plane half of Primitive_Intersect (scene.cpp:171-185).
-__device__ __forceinline__ float plane_cand(float4 g, const ray3 &r)
-{
-    const float d = g.x * r.d.x + g.y * r.d.y + g.z * r.d.z;
-    float cand = __builtin_inff();
-    if (d != 0) {
-        const float t = -((g.x * r.o.x + g.y * r.o.y + g.z * r.o.z) + g.w) / d;
-        if (t > 0) cand = t;
-    }
-    return cand;
-}
-
-// plane_cand without branches: the division for every lane, its result kept
-// only where the reference divides (d != 0) and t > 0.
+// Plane half of Primitive_Intersect (scene.cpp:171-185), without branches:
+// the division for every lane, its result kept only where the reference
+// divides (d != 0) and t > 0.
 __device__ __forceinline__ float plane_cand_lean(float4 g, const ray3 &r)
 {
     const float d = g.x * r.d.x + g.y * r.d.y + g.z * r.d.z;
@@ -142,15 +121,97 @@ struct Hit {
 
 struct Counts { unsigned long long traced, shadow, tests, tir; };
 
-// Engine_Raytrace, raytracer.cpp:30-271 (a_Depth is always 1 at every call
-// site, so the TRACEDEPTH guards are constant-true).
-// ocl: the device twin of openCLcode.h:150-390 -- a light hit adds the
-// light's colour (openCLcode.h:176-182) instead of (1,1,1); all else equal.
-// COUNT = false: the work counters are dead, so a shadow test stops as soon
-// as every lane of the wave has found an occluder (the reference's own early
-// exit, at wave granularity); only "occluded or not" is used then.
+// Engine_Raytrace's nearest hit (raytracer.cpp:39-49: min distance below 1e6,
+// lowest index on ties) for R rays per lane in lock-step: each sphere and
+// plane record is read once for all of them and their dependency chains
+// interleave (R = 2 in the latency-bound root kernel).  Branch-lean: a
+// sphere is one wave-uniform branch (skipped when no lane's det is
+// positive) around a straight-line body -- sqrt_nr for every lane, its range
+// checked once per loop, a lane outside it redoing its ray with the exact
+// per-sphere test -- and a plane test is straight-line (the division for
+// every lane, kept where the reference divides).  det <= 0 or NaN needs no
+// test of its own: sqrt_nr returns NaN there, so i2 > 0 fails.  (The
+// per-lane-branch forms cost more exec-mask instructions than VALU:
+// profiles/r04/whitted_lean_loops_ab.log.)  prim = 0x7fffffff: no hit.
+template <int R>
+__device__ __forceinline__ void nearest_n(const Scene &S, const ray3 (&ray)[R], float (&dist)[R], int (&prim)[R],
+                                          int (&result)[R])
+{
+    bool bad[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        dist[r] = 1000000.0f;
+        prim[r] = 0x7fffffff;
+        result[r] = 0;
+        bad[r] = false;
+    }
+    for (int k = 0; k < S.ns; k++) {
+        const float4 g = S.sph[k];
+        float b[R], det[R];
+        bool anyp = false;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const float vx = ray[r].o.x - g.x, vy = ray[r].o.y - g.y, vz = ray[r].o.z - g.z;
+            b[r] = vx * ray[r].d.x + vy * ray[r].d.y + vz * ray[r].d.z;
+            b[r] = -b[r];
+            det[r] = (b[r] * b[r]) - (vx * vx + vy * vy + vz * vz) + g.w;
+            anyp = anyp || det[r] > 0;
+        }
+        if (wave_any(anyp)) {
+            const int id = S.sph_id[k];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const float sd = sqrt_nr(det[r]);
+                bad[r] = bad[r] || (det[r] > 0 && !sqrt_nr_ok(det[r]));
+                const float i1 = b[r] - sd, i2 = b[r] + sd;
+                const float c = i1 < 0 ? i2 : i1;
+                const bool take = i2 > 0 && (c < dist[r] || (c == dist[r] && id < prim[r]));
+                dist[r] = take ? c : dist[r];
+                prim[r] = take ? id : prim[r];
+                result[r] = take ? (i1 < 0 ? -1 : 1) : result[r];
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        if (wave_any(bad[r])) {                         // (rare: det outside sqrt_nr's range)
+            dist[r] = 1000000.0f;
+            prim[r] = 0x7fffffff;
+            result[r] = 0;
+            for (int k = 0; k < S.ns; k++) {
+                int res;
+                const float c = sphere_cand(S.sph[k], ray[r], res);
+                const int id = S.sph_id[k];
+                if (res && (c < dist[r] || (c == dist[r] && id < prim[r]))) { dist[r] = c; prim[r] = id; result[r] = res; }
+            }
+        }
+    }
+#pragma unroll 4
+    for (int k = 0; k < S.np; k++) {
+        const float4 g = S.pln[k];
+        const int id = S.pln_id[k];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const float c = plane_cand_lean(g, ray[r]);
+            const bool take = c < dist[r] || (c == dist[r] && id < prim[r]);
+            dist[r] = take ? c : dist[r];
+            prim[r] = take ? id : prim[r];
+            result[r] = take ? 1 : result[r];
+        }
+    }
+}
+
+// The rest of Engine_Raytrace (raytracer.cpp:51-271) from its nearest hit
+// (a_Depth is always 1 at every call site, so the TRACEDEPTH guards are
+// constant-true).  ocl: the device twin of openCLcode.h:150-390 -- a light
+// hit adds the light's colour (openCLcode.h:176-182) instead of (1,1,1);
+// all else equal.  COUNT = false: the work counters are dead, so a shadow
+// test stops as soon as every lane of the wave has found an occluder (the
+// reference's own early exit, at wave granularity); only "occluded or not"
+// is used then.
 template <bool COUNT>
-__device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &cnt, bool ocl)
+__device__ Hit shade_hit(const Scene &S, const ray3 &ray, float rindex_in, float dist, int prim, int result,
+                         Counts &cnt, bool ocl)
 {
     Hit h;
     h.acc = mk(0.f, 0.f, 0.f);
@@ -159,59 +220,6 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
     h.refr_ray_ok = false;
     h.rindex_out = rindex_in;
     cnt.traced++;
-    // :39-49 nearest hit: min distance below 1e6, lowest index on ties.
-    float dist = 1000000.0f;
-    int prim = 0x7fffffff, result = 0;
-    bool bad = !(RT_WH_LEAN & 1);
-    if (RT_WH_LEAN & 1) {
-        // sphere_cand as one wave-uniform branch over a straight-line body
-        // (sqrt_nr for every lane, its range checked once per loop): the
-        // nested per-lane branches cost more mask instructions than VALU.
-        // det <= 0 or NaN needs no test of its own: sqrt_nr returns NaN
-        // there (v_rsq of a negative, 0 x inf at zero), so i2 > 0 fails.
-        for (int k = 0; k < S.ns; k++) {
-            const float4 g = S.sph[k];
-            const float vx = ray.o.x - g.x, vy = ray.o.y - g.y, vz = ray.o.z - g.z;
-            float b = vx * ray.d.x + vy * ray.d.y + vz * ray.d.z;
-            b = -b;
-            const float det = (b * b) - (vx * vx + vy * vy + vz * vz) + g.w;
-            if (wave_any(det > 0)) {
-                const float sd = sqrt_nr(det);
-                bad = bad || (det > 0 && !sqrt_nr_ok(det));
-                const float i1 = b - sd, i2 = b + sd;
-                const float c = i1 < 0 ? i2 : i1;
-                const int id = S.sph_id[k];
-                const bool take = i2 > 0 && (c < dist || (c == dist && id < prim));
-                dist = take ? c : dist;
-                prim = take ? id : prim;
-                result = take ? (i1 < 0 ? -1 : 1) : result;
-            }
-        }
-    }
-    if (wave_any(bad)) {                                // (rare: det outside sqrt_nr's range)
-        dist = 1000000.0f;
-        prim = 0x7fffffff;
-        result = 0;
-        for (int k = 0; k < S.ns; k++) {
-            int res;
-            const float c = sphere_cand(S.sph[k], ray, res);
-            const int id = S.sph_id[k];
-            if (res && (c < dist || (c == dist && id < prim))) { dist = c; prim = id; result = res; }
-        }
-    }
-#pragma unroll 4
-    for (int k = 0; k < S.np; k++) {
-        const float c = (RT_WH_LEAN & 2) ? plane_cand_lean(S.pln[k], ray) : plane_cand(S.pln[k], ray);
-        const int id = S.pln_id[k];
-        if (RT_WH_LEAN & 2) {
-            const bool take = c < dist || (c == dist && id < prim);
-            dist = take ? c : dist;
-            prim = take ? id : prim;
-            result = take ? 1 : result;
-        } else if (c < dist || (c == dist && id < prim)) {
-            dist = c; prim = id; result = 1;
-        }
-    }
     const int hit_once = prim != 0x7fffffff;
     if (!hit_once) prim = 0;
     cnt.tests += (unsigned long long)S.n;
@@ -265,24 +273,24 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
             // Any non-light primitive nearer than the light centre shades the
             // point (the reference breaks at the first one; which one does not
             // matter, only the count of tests, recovered from its position).
+            // The loops are nearest_n's lean forms.  (An all-occluded exit
+            // after each sphere measured slower; the planes take one
+            // all-occluded check before their loop.)
             int first = 0x7fffffff;
-            bool sbad = !(RT_WH_LEAN & 1);
-            if (RT_WH_LEAN & 1) {
-                for (int k = 0; k < S.nos; k++) {
-                    const float4 g = S.osph[k];
-                    const float vx = r.o.x - g.x, vy = r.o.y - g.y, vz = r.o.z - g.z;
-                    float b = vx * r.d.x + vy * r.d.y + vz * r.d.z;
-                    b = -b;
-                    const float det = (b * b) - (vx * vx + vy * vy + vz * vz) + g.w;
-                    if (wave_any(det > 0)) {
-                        const float sd = sqrt_nr(det);
-                        sbad = sbad || (det > 0 && !sqrt_nr_ok(det));
-                        const float i1 = b - sd, i2 = b + sd;
-                        const float c = i1 < 0 ? i2 : i1;
-                        const bool occ = i2 > 0 && c < tdist;
-                        first = occ ? min(first, S.osph_pos[k]) : first;
-                        if (!COUNT && RT_SPHERE_EXIT && !wave_any(first == 0x7fffffff)) break;
-                    }
+            bool sbad = false;
+            for (int k = 0; k < S.nos; k++) {
+                const float4 g = S.osph[k];
+                const float vx = r.o.x - g.x, vy = r.o.y - g.y, vz = r.o.z - g.z;
+                float b = vx * r.d.x + vy * r.d.y + vz * r.d.z;
+                b = -b;
+                const float det = (b * b) - (vx * vx + vy * vy + vz * vz) + g.w;
+                if (wave_any(det > 0)) {
+                    const float sd = sqrt_nr(det);
+                    sbad = sbad || (det > 0 && !sqrt_nr_ok(det));
+                    const float i1 = b - sd, i2 = b + sd;
+                    const float c = i1 < 0 ? i2 : i1;
+                    const bool occ = i2 > 0 && c < tdist;
+                    first = occ ? min(first, S.osph_pos[k]) : first;
                 }
             }
             if (wave_any(sbad)) {
@@ -297,10 +305,8 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
             const bool pl_any = COUNT || wave_any(first == 0x7fffffff);   // (all occluded by a sphere: no plane test)
 #pragma unroll 4
             for (int k = 0; pl_any && k < S.nop; k++) {
-                if (!COUNT && !RT_PLANE_ONECHECK && !wave_any(first == 0x7fffffff)) break;
-                const float c = (RT_WH_LEAN & 2) ? plane_cand_lean(S.opln[k], r) : plane_cand(S.opln[k], r);
-                if (RT_WH_LEAN & 2) first = c < tdist ? min(first, S.opln_pos[k]) : first;
-                else if (c < tdist) first = min(first, S.opln_pos[k]);
+                const float c = plane_cand_lean(S.opln[k], r);
+                first = c < tdist ? min(first, S.opln_pos[k]) : first;
             }
             if (first != 0x7fffffff) shade = 0;
             cnt.tests += (unsigned long long)(first != 0x7fffffff ? first + 1 : S.nnonlight);
@@ -356,6 +362,17 @@ __device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &c
         h.refl_ray.d = R;
     }
     return h;
+}
+
+// Engine_Raytrace, raytracer.cpp:30-271.
+template <bool COUNT>
+__device__ Hit trace(const Scene &S, const ray3 &ray, float rindex_in, Counts &cnt, bool ocl)
+{
+    const ray3 rr[1] = {ray};
+    float dist[1];
+    int prim[1], result[1];
+    nearest_n<1>(S, rr, dist, prim, result);
+    return shade_hit<COUNT>(S, ray, rindex_in, dist[0], prim[0], result[0], cnt, ocl);
 }
 
 // Primary ray of sub-sample `sub` (tx outer, ty inner: raytracer.cpp:351,364-367).
@@ -632,9 +649,15 @@ __device__ __forceinline__ SegView seg_view(const WfArgs &A, int L)
 #ifndef RT_WH_MINWAVES
 #define RT_WH_MINWAVES 6    // root/level kernels: occupancy 5 -> 6 (86 -> 79 VGPRs, no spills): -2 %
 #endif
+#ifndef RT_WH_ROOT_RAYS
+#define RT_WH_ROOT_RAYS 2   // root kernel: sub-sample rays per lane whose nearest hits are found together
+#endif
+#ifndef RT_WH_ROOT_MINWAVES
+#define RT_WH_ROOT_MINWAVES 6 // (R = 2: 80 VGPRs + 20 B scratch; 5 waves / 3 rays: level, profiles/r06/whitted_root_rays_ab.log)
+#endif
 
 template <bool COUNT>
-__global__ void __launch_bounds__(256, RT_WH_MINWAVES)
+__global__ void __launch_bounds__(256, RT_WH_ROOT_MINWAVES)
 root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float *__restrict__ sy_tab,
             float DX, float DY, unsigned long long *__restrict__ counters)
 {
@@ -655,25 +678,39 @@ root_kernel(WfArgs A, int row_end, const float *__restrict__ sx_tab, const float
     // are recorded for the later passes.
     float tr = 0.f, tg = 0.f, tb = 0.f;
     int kfirst = A.nsub;
-    for (int sub = 0; sub < A.nsub; sub++) {
-        Hit hh;
-        bool tir = false;
-        if (active) {
-            hh = trace<COUNT>(S, primary(sub, SX, SY, DX, DY, A.side), 1.0f, cnt, A.ocl);
-            tir = hh.refr > 0 && !hh.refr_ray_ok;
-            if (tir) cnt.tir++;
-        }
-        const int tree = sub * A.npix + pix;
-        const int wave_id = ((blockIdx.y * gridDim.x + blockIdx.x) << 2) + wave;
-        const int2 ch = queue_children(A, 0, 0, wave_id, active, tree, tree, 0, hh, tir);
-        if (active) {
-            if (kfirst == A.nsub && !(hh.refl > 0 || hh.refr > 0)) {
-                tr += hh.acc.x; tg += hh.acc.y; tb += hh.acc.z;
-            } else {
-                if (kfirst == A.nsub) kfirst = sub;
-                A.rcol[tree] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
-                A.rinfo[tree] = node_info(hh, tir);
-                A.rchild[tree] = ch;
+    const int wave_id = ((blockIdx.y * gridDim.x + blockIdx.x) << 2) + wave;
+    // The nearest hits of RT_WH_ROOT_RAYS sub-samples at a time (nearest_n:
+    // their chains interleave -- this pass is latency-bound), then each
+    // sub-sample shaded, recorded and queued in sub-sample order.
+    for (int sub0 = 0; sub0 < A.nsub; sub0 += RT_WH_ROOT_RAYS) {
+        ray3 rp[RT_WH_ROOT_RAYS];
+        float nd[RT_WH_ROOT_RAYS];
+        int np_[RT_WH_ROOT_RAYS], nr[RT_WH_ROOT_RAYS];
+#pragma unroll
+        for (int j = 0; j < RT_WH_ROOT_RAYS; j++) rp[j] = primary(min(sub0 + j, A.nsub - 1), SX, SY, DX, DY, A.side);
+        nearest_n<RT_WH_ROOT_RAYS>(S, rp, nd, np_, nr);
+#pragma unroll
+        for (int j = 0; j < RT_WH_ROOT_RAYS; j++) {
+            const int sub = sub0 + j;
+            if (sub >= A.nsub) break;                   // (uniform)
+            Hit hh;
+            bool tir = false;
+            if (active) {
+                hh = shade_hit<COUNT>(S, rp[j], 1.0f, nd[j], np_[j], nr[j], cnt, A.ocl);
+                tir = hh.refr > 0 && !hh.refr_ray_ok;
+                if (tir) cnt.tir++;
+            }
+            const int tree = sub * A.npix + pix;
+            const int2 ch = queue_children(A, 0, 0, wave_id, active, tree, tree, 0, hh, tir);
+            if (active) {
+                if (kfirst == A.nsub && !(hh.refl > 0 || hh.refr > 0)) {
+                    tr += hh.acc.x; tg += hh.acc.y; tb += hh.acc.z;
+                } else {
+                    if (kfirst == A.nsub) kfirst = sub;
+                    A.rcol[tree] = make_float4(hh.acc.x, hh.acc.y, hh.acc.z, hh.dist);
+                    A.rinfo[tree] = node_info(hh, tir);
+                    A.rchild[tree] = ch;
+                }
             }
         }
     }
