@@ -549,8 +549,7 @@ __device__ __forceinline__ void load_scene(Scene &S, const Scene *__restrict__ g
 // ---------------------------------------------------------------------------
 // Level pass.  count[] layout (zeroed per slab), one counter per 128-B line.
 constexpr int C_FIX = 0;                      // pixels listed for fix_kernel
-constexpr int C_DEEP = 1;                     // pixels listed for deep_kernel
-constexpr int C_BASE = 2;                     // + L: pool base of level L (2..5; level 1 at 0)
+constexpr int C_BASE = 1;                     // + L: pool base of level L (2..5; level 1 at 0)
 constexpr int C_SEG = C_BASE + LEVELS;        // + L * NSEG + s: length of segment s of level L (1..5)
 constexpr int C_TOTAL = C_SEG + LEVELS * lq::NSEG;
 #define QCNT(A, i) ((A).count[(i) * lq::CSTRIDE])
@@ -572,7 +571,6 @@ struct QArgs {
     unsigned *fixbits;    // [ntrees/32 + 1] tree whose records are incomplete or inexact
     unsigned *pixbits;    // [npix/32 + 1] pixel with such a tree: finished by fix_kernel
     int *fixlist;         // [fixcap] those pixels (fix_kernel scans pixbits when more)
-    int *deeplist;        // [npix] pixels of two or more recorded trees (final_kernel -> deep_kernel)
     // The record pool (levels 1..5), indexed by pool slot.
     float4 *ia;           // queued ray: o.xyz, d.x
     float4 *ib;           // d.y, d.z, weight, tree (bits)
@@ -777,20 +775,23 @@ level_kernel(QArgs A, int L)
 #define RT_Q_FOLD 8         // records per batch of the fold's breadth-first walk (A/B: 2,4,6,8,12,16 -> 8 best)
 #endif
 constexpr int FOLD = RT_Q_FOLD;
+#ifndef RT_Q_FOLD_ROOTS
+#define RT_Q_FOLD_ROOTS 9   // final_kernel: trees whose root records are read together (all nine; A/B: 1, 3, 5)
+#endif
 
-// ring(k): the walk's k-th queued slot (k taken mod RING), in LDS.
-template <bool COUNT, class Ring>
-__device__ __forceinline__ void fold_tree_from(const QArgs &A, float4 c0, int2 ch, Ring ring, float &ax, float &ay,
-                                               float &az, unsigned long long (&cnt)[4])
+template <bool COUNT, int COLS>
+__device__ __forceinline__ void fold_tree_from(const QArgs &A, float4 c0, int2 ch, int (*ring)[COLS], float &ax,
+                                               float &ay, float &az, unsigned long long (&cnt)[4])
 {
+    const int t = threadIdx.x;
     ax += c0.x; ay += c0.y; az += c0.z;
     const auto count = [&](unsigned cw) {
         cnt[0] += 1; cnt[1] += (cw >> 16) & 0xff; cnt[2] += cw & 0xffff; cnt[3] += cw >> 24;
     };
     if (COUNT) count(__float_as_uint(c0.w));
     int head = 0, tail = 0;
-    if (ch.x >= 0) ring(tail++) = ch.x;
-    if (ch.y >= 0) ring(tail++) = ch.y;
+    if (ch.x >= 0) ring[tail++ & (RING - 1)][t] = ch.x;
+    if (ch.y >= 0) ring[tail++ & (RING - 1)][t] = ch.y;
     for (int lvl = 1; head != tail; lvl++) {
         const int end = tail;                       // level lvl: entries [head, end)
         const bool inner = lvl < LEVELS - 1;
@@ -799,7 +800,7 @@ __device__ __forceinline__ void fold_tree_from(const QArgs &A, float4 c0, int2 c
             float4 c[FOLD];
             int2 cc[FOLD];
 #pragma unroll
-            for (int i = 0; i < FOLD; i++) q[i] = head + i < end ? ring(head + i) : -1;
+            for (int i = 0; i < FOLD; i++) q[i] = head + i < end ? ring[(head + i) & (RING - 1)][t] : -1;
 #pragma unroll
             for (int i = 0; i < FOLD; i++) {
                 if (q[i] >= 0) {
@@ -812,8 +813,8 @@ __device__ __forceinline__ void fold_tree_from(const QArgs &A, float4 c0, int2 c
                 if (q[i] < 0) break;
                 ax += c[i].x; ay += c[i].y; az += c[i].z;
                 if (COUNT) count(__float_as_uint(c[i].w));
-                if (cc[i].x >= 0) ring(tail++) = cc[i].x;
-                if (cc[i].y >= 0) ring(tail++) = cc[i].y;
+                if (cc[i].x >= 0) ring[tail++ & (RING - 1)][t] = cc[i].x;
+                if (cc[i].y >= 0) ring[tail++ & (RING - 1)][t] = cc[i].y;
                 head++;
             }
         }
@@ -826,9 +827,7 @@ template <bool COUNT, int COLS>
 __device__ __forceinline__ void fold_tree(const QArgs &A, int tree, int (*ring)[COLS], float &ax, float &ay,
                                           float &az, unsigned long long (&cnt)[4])
 {
-    const int t = threadIdx.x;
-    fold_tree_from<COUNT>(A, A.rcol[tree], A.rchild[tree], [&](int k) -> int & { return ring[k & (RING - 1)][t]; },
-                          ax, ay, az, cnt);
+    fold_tree_from<COUNT, COLS>(A, A.rcol[tree], A.rchild[tree], ring, ax, ay, az, cnt);
 }
 
 // :436-447: (int) as x86 converts (an overflowing or NaN sum packs 0), 255
@@ -844,19 +843,6 @@ __device__ __forceinline__ uint32_t pack_pixel(float ax, float ay, float az)
 
 // The pixel's sum in the reference's order and the pack, for every pixel
 // whose trees' records are complete and exact (the others: fix_kernel).
-//
-// The sum is one float chain over the pixel's recorded trees in order, each
-// tree's nodes breadth-first (:317-447).  A pixel looking into the glass
-// spheres records up to nine trees of up to five levels, and every level of
-// a tree is a dependent round of record loads (its child slots come from the
-// level above): walked by one lane, ~55 dependent rounds -- the kernel's
-// whole critical path, since such pixels cover whole tiles.  So the fold is
-// split by that depth: final_kernel (a lane per pixel) sums the pixels with
-// at most one recorded tree and lists the others (wave-aggregated append);
-// deep_kernel gives each listed pixel nine lanes, one per tree.
-#ifndef RT_Q_DEEP_MIN
-#define RT_Q_DEEP_MIN 10    // recorded trees from which a pixel is listed for deep_kernel (10: none)
-#endif
 template <bool COUNT>
 __global__ void __launch_bounds__(256)
 final_kernel(QArgs A, int row_end, uint32_t *__restrict__ out, unsigned long long *__restrict__ counters)
@@ -868,140 +854,31 @@ final_kernel(QArgs A, int row_end, uint32_t *__restrict__ out, unsigned long lon
     const int y = slab_row(A, r);
     unsigned long long cnt[4] = {0, 0, 0, 0};
     const int pix = r * A.w + x;
-    const bool valid = x < A.w && y < row_end && !pix_flagged(A, pix);
-    float4 ps = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (valid) ps = A.psum[pix];
-    const int kfirst = __float_as_int(ps.w);
-    const bool deep = valid && kfirst <= NSUB - RT_Q_DEEP_MIN;
-    const int pos = lq::wave_alloc(&QCNT(A, C_DEEP), deep ? 1 : 0);
-    if (deep) A.deeplist[pos] = pix;
-    if (valid && !deep) {
+    if (x < A.w && y < row_end && !pix_flagged(A, pix)) {
+        const float4 ps = A.psum[pix];
         float ax = ps.x, ay = ps.y, az = ps.z;
-        for (int sub = kfirst; sub < NSUB; sub++) fold_tree<COUNT, 256>(A, sub * A.npix + pix, ring, ax, ay, az, cnt);
-        out[(size_t)y * A.w + x] = pack_pixel(ax, ay, az);
-    }
-    if (COUNT) flush_counters<4>(counters, cnt);
-}
-
-// The listed pixels: nine lanes per pixel (seven pixels per wave) walk the
-// pixel's nine trees at once, breadth-first, each into its own LDS column --
-// an entry holds a pending child slot until its record arrives, then the
-// node's term: the column IS the walk's queue, in visiting order -- so a
-// pixel takes as many dependent rounds as its deepest tree.  After a
-// workgroup barrier the pixel's first lane adds the columns' terms to the
-// chain, tree by tree, in order: the reference's float additions, on terms
-// read from LDS.  A tree of more than FOLD_COL nodes is folded by that lane
-// from its records instead (fold_tree_from, the tree's column as the ring).
-// Counters (integers) are summed per lane, in any order.  Grid-stride over
-// the list (its length is known only on the device).
-#ifndef RT_Q_FOLD_COL
-#define RT_Q_FOLD_COL 8     // LDS entries per tree (16 B each): 32 KB per 256-thread block
+#if RT_Q_FOLD_ROOTS > 1
+        // The root records of RT_Q_FOLD_ROOTS trees loaded together (one
+        // latency instead of one per tree), then each tree folded in order.
+        constexpr int T = RT_Q_FOLD_ROOTS;
+        for (int s0 = __float_as_int(ps.w); s0 < NSUB; s0 += T) {
+            float4 c0[T];
+            int2 ch[T];
+#pragma unroll
+            for (int j = 0; j < T; j++) {
+                const int tree = (s0 + j < NSUB ? s0 + j : s0) * A.npix + pix;
+                c0[j] = A.rcol[tree];
+                ch[j] = A.rchild[tree];
+            }
+#pragma unroll
+            for (int j = 0; j < T; j++)
+                if (s0 + j < NSUB) fold_tree_from<COUNT, 256>(A, c0[j], ch[j], ring, ax, ay, az, cnt);
+        }
+#else
+        for (int sub = __float_as_int(ps.w); sub < NSUB; sub++)
+            fold_tree<COUNT, 256>(A, sub * A.npix + pix, ring, ax, ay, az, cnt);
 #endif
-constexpr int FOLD_COL = RT_Q_FOLD_COL;
-static_assert(FOLD_COL * 4 >= RING, "an overflowing tree's fold uses its column as the ring");
-
-template <bool COUNT>
-__global__ void __launch_bounds__(256)
-deep_kernel(QArgs A, uint32_t *__restrict__ out, unsigned long long *__restrict__ counters)
-{
-    __shared__ float4 col[FOLD_COL][256];
-    __shared__ int ncol[256];                         // entries of the lane's tree (-1: overflowed, fold it)
-    const int ndeep = QCNT(A, C_DEEP);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int t = threadIdx.x;
-    const int sub = lane % NSUB;
-    unsigned long long cnt[4] = {0, 0, 0, 0};
-    for (int base = (int)blockIdx.x * 28; base < ndeep; base += (int)gridDim.x * 28) {   // (uniform per block)
-        const int k = base + wave * 7 + lane / NSUB;
-        const bool pvalid = lane < 63 && k < ndeep;
-        int pix = 0;
-        float4 ps = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (pvalid) {
-            pix = A.deeplist[k];
-            ps = A.psum[pix];
-        }
-        int n = 0;
-        if (pvalid && sub >= __float_as_int(ps.w)) {
-            const int tree = sub * A.npix + pix;
-            const float4 c0 = A.rcol[tree];
-            const int2 ch = A.rchild[tree];
-            unsigned long long tc[4] = {0, 0, 0, 0};
-            const auto count = [&](unsigned cw) {
-                tc[0] += 1; tc[1] += (cw >> 16) & 0xff; tc[2] += cw & 0xffff; tc[3] += cw >> 24;
-            };
-            if (COUNT) count(__float_as_uint(c0.w));
-            col[0][t] = c0;
-            n = 1;
-            if (ch.x >= 0) col[n++][t].w = __int_as_float(ch.x);
-            if (ch.y >= 0) col[n++][t].w = __int_as_float(ch.y);
-            int head = 1;
-            for (int lvl = 1; head < n && n >= 0; lvl++) {
-                const int end = n;                  // level lvl: entries [head, end)
-                const bool inner = lvl < LEVELS - 1;
-                while (head < end && n >= 0) {
-                    int q[FOLD];
-                    float4 c[FOLD];
-                    int2 cc[FOLD];
-#pragma unroll
-                    for (int i = 0; i < FOLD; i++) q[i] = head + i < end ? __float_as_int(col[head + i][t].w) : -1;
-#pragma unroll
-                    for (int i = 0; i < FOLD; i++) {    // (past the level: slot 0, a valid record, unused)
-                        const int qq = q[i] >= 0 ? q[i] : 0;
-                        c[i] = A.ncol[qq];
-                        cc[i] = inner ? A.nchild[2 * qq] : make_int2(-1, -1);
-                    }
-#pragma unroll
-                    for (int i = 0; i < FOLD; i++) {
-                        if (q[i] >= 0 && n >= 0) {
-                            col[head][t] = c[i];
-                            if (COUNT) count(__float_as_uint(c[i].w));
-                            const int nc = (cc[i].x >= 0) + (cc[i].y >= 0);
-                            if (n + nc > FOLD_COL) {
-                                n = -1;             // overflow: this tree is folded from its records
-                            } else {
-                                if (cc[i].x >= 0) col[n++][t].w = __int_as_float(cc[i].x);
-                                if (cc[i].y >= 0) col[n++][t].w = __int_as_float(cc[i].y);
-                                head++;
-                            }
-                        }
-                    }
-                }
-            }
-            if (COUNT && n >= 0)
-                for (int j = 0; j < 4; j++) cnt[j] += tc[j];
-        }
-        ncol[t] = n;
-        __syncthreads();
-        if (pvalid && sub == 0) {                   // the pixel's first lane: the chain, tree by tree
-            float ax = ps.x, ay = ps.y, az = ps.z;
-            for (int s = __float_as_int(ps.w); s < NSUB; s++) {
-                const int ts = t + s;
-                const int ns = ncol[ts];
-                if (ns < 0) {                       // (its column, FOLD_COL x 16 B, as the RING-slot ring)
-                    const int tree = s * A.npix + pix;
-                    fold_tree_from<COUNT>(
-                        A, A.rcol[tree], A.rchild[tree],
-                        [&](int k) -> int & { return ((int *)&col[(k & (RING - 1)) >> 2][ts])[k & 3]; }, ax, ay, az,
-                        cnt);
-                    continue;
-                }
-                int j = 0;
-                for (; j + 4 <= ns; j += 4) {      // (four LDS reads in flight, then the adds in order)
-                    const float4 a0 = col[j][ts], a1 = col[j + 1][ts], a2 = col[j + 2][ts], a3 = col[j + 3][ts];
-                    ax += a0.x; ay += a0.y; az += a0.z;
-                    ax += a1.x; ay += a1.y; az += a1.z;
-                    ax += a2.x; ay += a2.y; az += a2.z;
-                    ax += a3.x; ay += a3.y; az += a3.z;
-                }
-                for (; j < ns; j++) {
-                    const float4 a0 = col[j][ts];
-                    ax += a0.x; ay += a0.y; az += a0.z;
-                }
-            }
-            const int x = pix % A.w, y = slab_row(A, pix / A.w);
-            out[(size_t)y * A.w + x] = pack_pixel(ax, ay, az);
-        }
-        __syncthreads();                            // (the columns are reused by the next pixels)
+        out[(size_t)y * A.w + x] = pack_pixel(ax, ay, az);
     }
     if (COUNT) flush_counters<4>(counters, cnt);
 }
@@ -1145,7 +1022,7 @@ int arena(rtrt::DeviceState &st, int slot, int w, int rows, rt::queue::QArgs *A)
     const size_t FB = (T + 31) / 32 * 4, PB = (npix + 31) / 32 * 4;
     const size_t FC = std::max<size_t>(npix / 64, 4096);       // listed pixels (fix_kernel)
     const size_t bytes = al(sizeof(Scene)) + al(T * 16) + al(T * 8) + al(npix * 16) + al(FB) + al(PB) +
-                         al(FC * 4) + al(npix * 4) + al(P * 16) * 3 + al(sizeof(int) * C_TOTAL * rt::lq::CSTRIDE);
+                         al(FC * 4) + al(P * 16) * 3 + al(sizeof(int) * C_TOTAL * rt::lq::CSTRIDE);
     if (st.cap[slot] < bytes && st.wf_pending) {
         int rc = wait_frame(st);
         if (rc) return rc;
@@ -1162,7 +1039,6 @@ int arena(rtrt::DeviceState &st, int slot, int w, int rows, rt::queue::QArgs *A)
     A->fixbits = (unsigned *)take(FB);
     A->pixbits = (unsigned *)take(PB);
     A->fixlist = (int *)take(FC * 4);
-    A->deeplist = (int *)take(npix * 4);
     A->ia = (float4 *)take(P * 16);
     A->ib = (float4 *)take(P * 16);
     A->ic = (float4 *)take(P * 16);
@@ -1197,9 +1073,7 @@ int launch(const rt::queue::QArgs &A, int w, int rows, int row_end, float DX, fl
     hipLaunchKernelGGL((root_kernel<COUNT, UNCERT>), tiles, block, 0, s, A, row_end, DX, DY, cnt);
     for (int L = 1; L < LEVELS; L++)
         hipLaunchKernelGGL((level_kernel<COUNT, UNCERT>), dim3(level_blocks), block, 0, s, A, L);
-    static const int deep_blocks = resident_blocks(deep_kernel<COUNT>);
     hipLaunchKernelGGL(final_kernel<COUNT>, tiles, block, 0, s, A, row_end, d_px, cnt);
-    hipLaunchKernelGGL(deep_kernel<COUNT>, dim3(deep_blocks), block, 0, s, A, d_px, cnt);
     hipLaunchKernelGGL(fix_kernel<COUNT>, dim3(256), dim3(64), 0, s, A, DX, DY, d_px, cnt);
     return rtrt::check_launch("rtq kernels");
 }
