@@ -149,9 +149,14 @@ def test_large_scene_global_path(rt, oracle, env, monkeypatch):
 
 
 # The two hierarchy walks: the 8-wide LDS-resident tree (default for scenes
-# whose tree fits a block's LDS) and the binary octant-layout tree in global
-# memory (RT_SPT_WIDE=0; the path for larger trees).
-WALKS = [pytest.param({}, id="wide"), pytest.param({"RT_SPT_WIDE": "0"}, id="binary")]
+# whose tree fits a block's LDS; its uncounted launches learn a tile-group
+# order) -- also with a learnt pixel order instead (psort=1 global, 2 inside
+# each group; exact, slower, kept for A/B) -- and the binary
+# octant-layout tree in global memory (RT_SPT_WIDE=0; the path for larger
+# trees).
+WALKS = [pytest.param({}, id="wide"), pytest.param({"RT_SPT_TUNE": "psort=1"}, id="wide-pixelorder"),
+         pytest.param({"RT_SPT_TUNE": "psort=2"}, id="wide-pixelorder-local"),
+         pytest.param({"RT_SPT_WIDE": "0"}, id="binary")]
 
 
 @pytest.mark.parametrize("walk", WALKS)
@@ -171,12 +176,13 @@ def test_configs4_full_size_golden(rt, oracle, counted, walk, monkeypatch):
     spheres, n, cam = rt.scenes.complex10k()
     w, h = 1920, 1080
     rt.scenes.update_camera(cam, w, h)
-    f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n, camera=cam)
-    f.render(64, counters=counted)
-    got = (oracle.fnv1a64(f.colors), oracle.fnv1a64(f.pixels), oracle.fnv1a64(f.seeds))
-    assert got == (g["colors"], g["pixels"], g["seeds"])
-    if counted:
-        assert f.counters[3] == w * h * 64
+    for frame in range(3):          # (the 1st launch of the key learns its order, later ones use it)
+        f = rt.SmallptFrame(w, h, spheres=spheres, nspheres=n, camera=cam)
+        f.render(64, counters=counted)
+        got = (oracle.fnv1a64(f.colors), oracle.fnv1a64(f.pixels), oracle.fnv1a64(f.seeds))
+        assert got == (g["colors"], g["pixels"], g["seeds"]), frame
+        if counted:
+            assert f.counters[3] == w * h * 64
 
 
 @pytest.mark.parametrize("coop", ["512", "4096"])

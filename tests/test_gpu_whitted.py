@@ -216,7 +216,7 @@ def test_pool_grows_after_overflow(rt, oracle, monkeypatch):
 def test_sphere_loop_exact_redo(rt, oracle):
     """trace()'s sphere loops use sqrt_nr for every lane and redo the whole
     loop with the exact per-sphere test when some lane's discriminant is
-    outside its range (whitted.hip RT_WH_LEAN).  A non-light sphere of
+    outside its range (whitted.hip nearest_n, shade_hit).  A non-light sphere of
     infinite radius makes every discriminant +inf -- never a hit, but a redo
     in every nearest and occluder loop: frame and counters stay the
     oracle's."""
