@@ -1230,7 +1230,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
               const float4 *__restrict__ g_geo, const float4 *__restrict__ g_emi,
               const float4 *__restrict__ g_col, const float4 *__restrict__ g_lrec, int nlights,
               BvhView bvh, unsigned long long *__restrict__ counters, int *__restrict__ work, int split,
-              int nheavy, int sflags, const int *__restrict__ pix_order, unsigned *__restrict__ pix_cost)
+              int nheavy, int sflags)
 {
     constexpr bool LDS = GEO == GEO_LDS;
     // GEO_WIDE: persistent waves -- each wave takes 8x8 tiles from a work
@@ -1357,21 +1357,9 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     // entries; a slot past it or an entry outside the frame renders nothing.
     const int grp = group_order ? (slot < nslots ? group_order[slot] : -1) : slot;
     const bool gvalid = (unsigned)grp < (unsigned)((ntiles + 3) >> 2);
-    const int tile0 = grp * 4 + (item & 3);
-    const int li0 = coop ? (sub << (6 - hs)) + (cg == 8 ? lane >> 3 : lane >> 2) : lane;   // pixel of the 8x8 tile
+    const int tile = grp * 4 + (item & 3);
+    const int li = coop ? (sub << (6 - hs)) + (cg == 8 ? lane >> 3 : lane >> 2) : lane;   // pixel of the 8x8 tile
     const bool lead = !coop || (lane & (cg - 1)) == 0;  // the lane that stores the pixel and counts
-    // pix_order (8-wide launches once a pixel order is learnt; group_order is
-    // then null): the window's pixels -- ids tile * 64 + pixel of the tile --
-    // in decreasing cost, 64 per work item, so a wave's lanes hold pixels of
-    // similar cost instead of an 8x8 tile's mix (sky beside the fractal:
-    // its lanes needed 0.72 of the tile's slowest pixel on average).  Only
-    // which lane runs a pixel changes, never its computation.
-    int tile = tile0, li = li0;
-    if (pix_order) {
-        const int wp = gvalid ? pix_order[item * 64 + li0] : 0;
-        tile = wp >> 6;
-        li = wp & 63;
-    }
     unsigned long long t_start = 0;
     if (SCHED) t_start = __builtin_amdgcn_s_memrealtime();
     // GSTORE (hierarchy kernels): per group of the block a 32x8 staging
@@ -1476,7 +1464,6 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
         for (int b = 0; b < 3; b++) walk.pf_l[b] = walk.pf_w[b] = 0;
 #endif
         bool walking = false;  //   and whether it is suspended mid-walk
-        unsigned pit = 0;      // loop iterations of this lane's pixel (pix_cost: the learning launch)
         constexpr float nc = 1.f, nt = 1.5f;
         // prio_sched: the three level boundaries as fractions of the samples
         // (8 bits each, in 1/256; host: prio_schedule).  Every wave starts at
@@ -1609,7 +1596,6 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             }
 
             SPT_PROF(PB_ITER);
-            pit++;
 #ifdef RT_SPT_TRACE
             tr_iters++;
 #endif
@@ -1938,7 +1924,6 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
             }
             seeds_out[2 * (size_t)i] = s0;
             seeds_out[2 * (size_t)i + 1] = s1;
-            if (pix_cost && active) pix_cost[tile * 64 + li] = pit;   // (the learning launch: its loop iterations)
         }
 #ifdef RT_SPT_PROF
         for (int b = 0; b < 3; b++) {
@@ -2147,14 +2132,6 @@ struct SptSched {
     // the scene, and a fresh buffer takes the next order.
     bool order_captured = false;
     std::vector<int *> retired;
-    // 8-wide scenes, uncounted launches (SptTune psort): the learning launch
-    // also records each window pixel's loop iterations, and later launches
-    // dispatch the pixels themselves in decreasing cost (pix_order) instead
-    // of the groups (256 window-pixel ids per slot: tile * 64 + pixel).
-    bool pix = false;                 // this key's order is a pixel order
-    int pcap = 0;
-    unsigned *d_pcost = nullptr, *h_pcost = nullptr;
-    int *d_perm = nullptr, *h_perm = nullptr;
 };
 
 struct spt_scene {
@@ -2215,15 +2192,11 @@ size_t wide_lds_bytes(int wnodes, int wdepth, int wpb, bool counted = true)
 //               (64/128/192 for the 4-wave block shape, 128/192/224 for 16)
 //   wpb=4|16    full-scan block shape (default: by waves of work per SIMD)
 //   blocks=N    8-wide persistent grid size (default: one block per CU)
-//   psort=0|1|2 uncounted 8-wide launches learn a pixel order instead of a
-//               group order: 1 all pixels in decreasing cost, 64 per wave;
-//               2 groups heaviest first, each group's pixels sorted inside it
 struct SptTune {
     int coop = -1, coop_g = 0, coop_waves = -1, routed = -1;
     int budget = 16, batch = 16, stop = 32;
     int prio[3] = {-1, -1, -1};
     int wpb = 0, blocks = 0;
-    int psort = 0;
 };
 SptTune spt_tune()
 {
@@ -2249,7 +2222,6 @@ SptTune spt_tune()
         else if (k == "prio") sscanf(v, "%d/%d/%d", &t.prio[0], &t.prio[1], &t.prio[2]);
         else if (k == "wpb") t.wpb = atoi(v) == 16 ? 16 : 4;
         else if (k == "blocks") t.blocks = std::max(atoi(v), 0);
-        else if (k == "psort") t.psort = std::min(std::max(atoi(v), 0), 2);
     }
     return t;
 }
@@ -2267,8 +2239,6 @@ struct Shape {
     unsigned *cost = nullptr;
     bool tiers = true;                // with order: its first tiles get the heavy-tile treatment
     bool cost_max = false;            // cost: a group's longest tile (atomic max), not the sum
-    const int *perm = nullptr;        // 8-wide: the learnt pixel order (render_kernel's pix_order), or
-    unsigned *pcost = nullptr;        //   the learning launch's per-pixel iteration counts (pix_cost)
     SptTune tune;
 };
 // Rows [r0, r1), or (gstride > 1) the 8-row groups r0/8, r0/8 + gstride, ...
@@ -2364,7 +2334,7 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
     // 18.0-19.8 -> 11.4-15.1 ms, N = 4 18.7 -> 17 ms; see DESIGN.md.
     const SptTune &tu = g.tune;
     int n1 = 0, n2 = 0, sp = 0, kcg = 0;
-    if (GEO == rt::smallpt::GEO_WIDE && (g.order || g.perm) && g.tiers) {
+    if (GEO == rt::smallpt::GEO_WIDE && g.order && g.tiers) {
         n2 = std::min(4 * g.nblocks, 4 * g.nslots);
         const double wps = (double)g.work / (4.0 * sc.cus);
         int hw = 0, cg = 8;
@@ -2408,7 +2378,7 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
     hipLaunchKernelGGL(kern, dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.nslots, g.gstride, first,
                        ns, prio_schedule(g), g.order, g.cost, gg, ge, gc, gl, sc.nlights, sc.bvh, cnt, work, split,
-                       nheavy, sflags, g.perm, g.pcost);
+                       nheavy, sflags);
     return RT_OK;
 }
 
@@ -2619,13 +2589,9 @@ extern "C" int spt_scene_destroy(spt_scene *sc)
         SptSched &q = *qp;
         if (q.d_cost) (void)hipFree(q.d_cost);
         if (q.d_order) (void)hipFree(q.d_order);
-        if (q.d_pcost) (void)hipFree(q.d_pcost);
-        if (q.d_perm) (void)hipFree(q.d_perm);
         for (int *p : q.retired) (void)hipFree(p);
         if (q.h_cost) (void)hipHostFree(q.h_cost);
         if (q.h_order) (void)hipHostFree(q.h_order);
-        if (q.h_pcost) (void)hipHostFree(q.h_pcost);
-        if (q.h_perm) (void)hipHostFree(q.h_perm);
         if (q.ev) (void)hipEventDestroy(q.ev);
     }
     delete sc;
@@ -2665,35 +2631,11 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
         if (q.state == 2) {                            // a device pointer, kept alive and unchanged from now on
-            if (q.pix) g.perm = q.d_perm;
-            else g.order = q.d_order;
+            g.order = q.d_order;
             q.order_captured = true;
         }
         return false;
     }
-    // A pixel order for the uncounted 8-wide launches (SptTune psort).
-    const bool want_pix = sc.bvh.wnode && !full_count && g.tune.psort;
-    const int npix_ids = 256 * nslots;
-    if (want_pix && npix_ids > q.pcap) {                // grow (the old buffers may still be read)
-        if (q.ev && hipEventSynchronize(q.ev) != hipSuccess) return false;
-        if (hipStreamSynchronize(s) != hipSuccess) return false;
-        if (q.d_pcost) (void)hipFree(q.d_pcost);
-        if (q.d_perm && q.order_captured) q.retired.push_back(q.d_perm);
-        else if (q.d_perm) (void)hipFree(q.d_perm);
-        if (q.h_pcost) (void)hipHostFree(q.h_pcost);
-        if (q.h_perm) (void)hipHostFree(q.h_perm);
-        q.d_pcost = q.h_pcost = nullptr;
-        q.d_perm = q.h_perm = nullptr;
-        q.pcap = 0;
-        q.state = 0;
-        if (hipMalloc(&q.d_pcost, sizeof(unsigned) * npix_ids) != hipSuccess ||
-            hipMalloc(&q.d_perm, sizeof(int) * npix_ids) != hipSuccess ||
-            hipHostMalloc(&q.h_pcost, sizeof(unsigned) * npix_ids) != hipSuccess ||
-            hipHostMalloc(&q.h_perm, sizeof(int) * npix_ids) != hipSuccess)
-            return false;
-        q.pcap = npix_ids;
-    }
-    if (q.state != 0 && q.pix != want_pix) q.state = 0;   // (the tuning changed: learn again)
     if (nslots > q.cap) {                               // grow (the old buffers may still be read)
         if (q.ev && hipEventSynchronize(q.ev) != hipSuccess) return false;
         if (hipStreamSynchronize(s) != hipSuccess) return false;
@@ -2715,41 +2657,7 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
         q.cap = nslots;
         q.state = 0;
     }
-    if (q.state == 1 && q.pix && hipEventQuery(q.ev) == hipSuccess) {
-        // Pixels in decreasing iteration count, ties in id order: a counting
-        // sort (O(n) for the 2 M ids of a 1080p window).
-        if (g.tune.psort == 2) {
-            // Local: groups heaviest first (their longest tile), each group's
-            // 256 pixels heaviest first inside it.
-            std::vector<int> idx(nslots);
-            for (int i = 0; i < nslots; i++) idx[i] = i;
-            std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return q.h_cost[a] > q.h_cost[b]; });
-            for (int k = 0; k < nslots; k++) {
-                int *dst = q.h_perm + (size_t)k * 256;
-                const unsigned *c = q.h_pcost + (size_t)idx[k] * 256;
-                for (int j = 0; j < 256; j++) dst[j] = idx[k] * 256 + j;
-                std::stable_sort(dst, dst + 256, [&](int a, int b) { return c[a & 255] > c[b & 255]; });
-            }
-        } else {
-            unsigned mx = 0;
-            for (int i = 0; i < npix_ids; i++) mx = std::max(mx, q.h_pcost[i]);
-            std::vector<int> start((size_t)mx + 2, 0);
-            for (int i = 0; i < npix_ids; i++) start[mx - q.h_pcost[i] + 1]++;
-            for (size_t c = 1; c < start.size(); c++) start[c] += start[c - 1];
-            for (int i = 0; i < npix_ids; i++) q.h_perm[start[mx - q.h_pcost[i]]++] = i;
-        }
-        if (q.order_captured) {                        // a graph reads the old order: keep it, take a new buffer
-            int *fresh = nullptr;
-            if (hipMalloc(&fresh, sizeof(int) * q.pcap) != hipSuccess) return false;
-            q.retired.push_back(q.d_perm);
-            q.d_perm = fresh;
-            q.order_captured = false;
-        }
-        if (hipMemcpyAsync(q.d_perm, q.h_perm, sizeof(int) * npix_ids, hipMemcpyHostToDevice, s) != hipSuccess)
-            return false;
-        q.state = 2;
-    }
-    if (q.state == 1 && !q.pix && hipEventQuery(q.ev) == hipSuccess) {
+    if (q.state == 1 && hipEventQuery(q.ev) == hipSuccess) {
         // heaviest first; ties (and the groups past the window: no tiles, 0)
         // in slot order
         std::vector<int> idx(nslots);
@@ -2768,18 +2676,12 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
         q.state = 2;
     }
     if (q.state == 2) {
-        if (q.pix) g.perm = q.d_perm;
-        else g.order = q.d_order;
+        g.order = q.d_order;
         return false;
     }
     if (q.state == 0) {
         if (hipMemsetAsync(q.d_cost, 0, sizeof(unsigned) * nslots, s) != hipSuccess) return false;
         g.cost = q.d_cost;
-        q.pix = want_pix;
-        if (want_pix) {
-            if (hipMemsetAsync(q.d_pcost, 0, sizeof(unsigned) * npix_ids, s) != hipSuccess) return false;
-            g.pcost = q.d_pcost;
-        }
         // The order key is a group's longest tile (its slowest pixel chain),
         // not the sum of its four: the heavy-tile treatment (cooperative or
         // routed tiles) goes to the first groups in order, and a group with
@@ -2794,12 +2696,9 @@ bool sched_before(const spt_scene &sc, Shape &g, hipStream_t s, int w, int h, in
 void sched_after(const spt_scene &sc, hipStream_t s, bool full_count)
 {
     SptSched &q = full_count ? sc.sched_cnt : sc.sched;
-    if (hipMemcpyAsync(q.h_cost, q.d_cost, sizeof(unsigned) * q.nslots, hipMemcpyDeviceToHost, s) != hipSuccess)
-        return;
-    if (q.pix && hipMemcpyAsync(q.h_pcost, q.d_pcost, sizeof(unsigned) * 256 * (size_t)q.nslots,
-                                hipMemcpyDeviceToHost, s) != hipSuccess)
-        return;
-    if (hipEventRecord(q.ev, s) == hipSuccess) q.state = 1;
+    if (hipMemcpyAsync(q.h_cost, q.d_cost, sizeof(unsigned) * q.nslots, hipMemcpyDeviceToHost, s) == hipSuccess &&
+        hipEventRecord(q.ev, s) == hipSuccess)
+        q.state = 1;
 }
 
 // One launch of rows [row_begin, row_end) (every gstride-th 8-row group), or

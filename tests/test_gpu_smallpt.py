@@ -149,14 +149,9 @@ def test_large_scene_global_path(rt, oracle, env, monkeypatch):
 
 
 # The two hierarchy walks: the 8-wide LDS-resident tree (default for scenes
-# whose tree fits a block's LDS; its uncounted launches learn a tile-group
-# order) -- also with a learnt pixel order instead (psort=1 global, 2 inside
-# each group; exact, slower, kept for A/B) -- and the binary
-# octant-layout tree in global memory (RT_SPT_WIDE=0; the path for larger
-# trees).
-WALKS = [pytest.param({}, id="wide"), pytest.param({"RT_SPT_TUNE": "psort=1"}, id="wide-pixelorder"),
-         pytest.param({"RT_SPT_TUNE": "psort=2"}, id="wide-pixelorder-local"),
-         pytest.param({"RT_SPT_WIDE": "0"}, id="binary")]
+# whose tree fits a block's LDS) and the binary octant-layout tree in global
+# memory (RT_SPT_WIDE=0; the path for larger trees).
+WALKS = [pytest.param({}, id="wide"), pytest.param({"RT_SPT_WIDE": "0"}, id="binary")]
 
 
 @pytest.mark.parametrize("walk", WALKS)
