@@ -1014,6 +1014,35 @@ __device__ __forceinline__ bool leaf_coop(const BvhView &B, const ray3 &r, bool 
     return false;
 }
 
+// The crossed leaves l1 of node n1 and l2 of node n2, RT_SPT_COOP_NL per
+// pass; true when an uncounted any-hit found an occluder.
+template <bool COUNT, int G, bool LOC>
+__device__ __forceinline__ bool coop_leaves(const BvhView &B, const ray3 &r, bool shadow, float maxt,
+                                            const unsigned *Lw, int oct, int n1, unsigned l1, int n2, unsigned l2,
+                                            int pos, int gbase, float &t, int &bpos, int &id)
+{
+    while (l1 | l2) {
+        int fa[RT_SPT_COOP_NL], ca[RT_SPT_COOP_NL];
+#pragma unroll
+        for (int q = 0; q < RT_SPT_COOP_NL; q++) {
+            fa[q] = ca[q] = 0;
+            if (l1 | l2) {
+                const bool first = l1 != 0;
+                const unsigned lq = first ? l1 : l2;
+                const int iq = __builtin_ctz(lq);
+                l1 = first ? (l1 & (l1 - 1u)) : l1;
+                l2 = first ? l2 : (l2 & (l2 - 1u));
+                const int wq = ~(int)Lw[(first ? n1 : n2) * WIDE_WORDS + 8 + (iq ^ oct)];
+                fa[q] = wq & 0xffffff;
+                ca[q] = wq >> 24;
+            }
+        }
+        if (leaf_coop<COUNT, G, RT_SPT_COOP_NL, LOC>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id))
+            return true;
+    }
+    return false;
+}
+
 template <bool COUNT, int G>
 __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, unsigned *__restrict__ stk,
                                const ray3 &r, bool shadow, BvhWalk &W, int opts)
@@ -1048,6 +1077,8 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
     // once per query instead of per leaf: N = 8 / 4 shares -2 to -3 %)
     constexpr bool LOC = G == 8;
     float tg = LOC ? grp_min<G>(t) : t;
+    unsigned pl = 0u;                           // the previous trip's crossed leaves (of node pn), pending
+    int pn = 0;
     while (true) {
         const bool has = m != 0;
         const int p = __builtin_ctz(m | 256u);
@@ -1074,30 +1105,23 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
                                                  lm);
         hm = vis ? hm : 0u;
         lm = vis ? lm : 0u;
-        if (wave_any(lm != 0)) {
+        // A trip's crossed leaves wait one trip, so one leaf section serves
+        // two trips' leaves of every group: the lone heavy wave of an N = 8
+        // share runs half as many leaf sections (~50 % of its chain).  Exact:
+        // the nearest hit is order-independent; the culling limit tg lags
+        // one trip.  N = 8 shares 9.8-10.1 -> 9.3-9.65 ms, N = 4 13.6-14.2
+        // -> 13.0-13.5 ms (profiles/r06/c4_coop_defer_ab.log).
+        bool run = wave_any(pl != 0);
+        if (!run && wave_any(lm != 0)) {
+            pl = lm;
+            pn = cv;
+        } else if (run) {
 #ifdef RT_SPT_TRACE
             const unsigned long long tr_l0 = __builtin_amdgcn_s_memtime();
             W.tr_leafruns++;
 #endif
-            unsigned l = lm;
-            while (l) {
-                int fa[RT_SPT_COOP_NL], ca[RT_SPT_COOP_NL];
-#pragma unroll
-                for (int q = 0; q < RT_SPT_COOP_NL; q++) {
-                    fa[q] = ca[q] = 0;
-                    if (l) {
-                        const int iq = __builtin_ctz(l);
-                        l &= l - 1;
-                        const int wq = ~(int)Lw[cv * WIDE_WORDS + 8 + (iq ^ oct)];
-                        fa[q] = wq & 0xffffff;
-                        ca[q] = wq >> 24;
-                    }
-                }
-                if (leaf_coop<COUNT, G, RT_SPT_COOP_NL, LOC>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id)) {
-                    occl = true;
-                    break;
-                }
-            }
+            occl = coop_leaves<COUNT, G, LOC>(B, r, shadow, maxt, Lw, oct, pn, pl, cv, lm, pos, gbase, t, bpos, id) || occl;
+            pl = 0u;
             if (LOC) tg = grp_min<G>(t);
 #ifdef RT_SPT_TRACE
             W.tr_leaf += (unsigned)(__builtin_amdgcn_s_memtime() - tr_l0);
@@ -1115,7 +1139,15 @@ __device__ bool wide_walk_coop(const BvhView &B, const uint4 *__restrict__ L, un
         m = pop ? (e2 & 255u) : m;
         trips++;
         const unsigned long long am = __builtin_amdgcn_ballot_w64(m != 0);
-        if (am == 0 || trips >= budget || 64 * __builtin_popcountll(am) <= stop * n0) break;
+        if (am == 0 || trips >= budget || 64 * __builtin_popcountll(am) <= stop * n0) {
+            if (wave_any(pl != 0)) {                    // (no leaf is left pending past the call)
+                if (coop_leaves<COUNT, G, LOC>(B, r, shadow, maxt, Lw, oct, pn, pl, 0, 0u, pos, gbase, t, bpos, id)) {
+                    m = 0u;
+                    sp = 0;
+                }
+            }
+            break;
+        }
     }
     if (LOC && m == 0 && !shadow) {
         // the group's result from its lanes' bests: the minimum distance,

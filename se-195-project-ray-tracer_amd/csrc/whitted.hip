@@ -918,9 +918,6 @@ backacc_kernel(WfArgs A, int L)
 // Level 0 of the pixel's nine trees, folded with the FD levels below it
 // (level FD's colours final), the sum over sub-samples (:513-515) and the
 // x28 / clamp / XRGB pack (:517-523).
-#ifndef RT_WH_FINAL_BATCH
-#define RT_WH_FINAL_BATCH 1     // 1: the nine root records read in one round (final_kernel<1> 39.6 -> 33.6 us); 0: a round per tree
-#endif
 template <int FD>
 __global__ void __launch_bounds__(256)
 final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
@@ -935,10 +932,10 @@ final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
     const int pix = r * A.w + x;
     const float4 ps = A.psum[pix];                          // the leading childless trees, summed by root_kernel
     float tr = ps.x, tg = ps.y, tb = ps.z;
-#if RT_WH_FINAL_BATCH
     // The root records of all the pixel's remaining trees read in one round
-    // (they do not depend on each other), then each tree's children and its
-    // share of the sum in sub-sample order.
+    // (they do not depend on each other; a round per tree: final_kernel<1>
+    // 39.6 us against 33.6), then each tree's children and its share of the
+    // sum in sub-sample order.
     constexpr int T = 9;                                   // nsub <= 9 (3 x 3; 2 x 2 for openCLcode.cl)
     const int kf = __float_as_int(ps.w);
     float4 c0[T];
@@ -968,22 +965,6 @@ final_kernel(WfArgs A, int row_end, uint32_t *__restrict__ out)
         }
         tr += c.x; tg += c.y; tb += c.z;
     }
-#else
-    for (int sub = __float_as_int(ps.w); sub < A.nsub; sub++) {
-        const int tree = sub * A.npix + pix;
-        float4 c0 = A.rcol[tree];
-        if (!flagged(A, tree)) {
-            const int2 ch = A.rchild[tree];
-            if (ch.x >= 0 || ch.y >= 0) {
-                const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-                const float4 cx = ch.x >= 0 ? folded<FD - 1>(A, S, ch.x) : z;
-                const float4 cy = ch.y >= 0 ? folded<FD - 1>(A, S, ch.y) : z;
-                c0 = accumulate(S, c0, A.rinfo[tree], ch, cx, cy, A.ocl);
-            }
-        }
-        tr += c0.x; tg += c0.y; tb += c0.z;
-    }
-#endif
     const float scale = A.ocl ? 64.0f : 28.0f;            // 256/4 (openCLcode.cl:238) or 256/9 (:517)
     int red = cvt_i32_x86(tr * scale), green = cvt_i32_x86(tg * scale), blue = cvt_i32_x86(tb * scale);
     if (red > 255) red = 255;

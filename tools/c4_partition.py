@@ -126,11 +126,18 @@ def main():
         # SWEEP="n1:hw,..." times the balanced lists under other heavy-tile
         # policies (RT_SPT_TUNE coop = cooperative tiles, coop_waves = waves
         # per block that fetch them first); "-" = the library default.
+        # TUNES="walk=32/16/32;coop=256" times them under whole RT_SPT_TUNE
+        # strings instead (';'-separated).
         tune0 = os.environ.get("RT_SPT_TUNE")
-        for pol in os.environ.get("SWEEP", "-").split(","):
-            if pol != "-":
+        pols = os.environ["TUNES"].split(";") if os.environ.get("TUNES") else os.environ.get("SWEEP", "-").split(",")
+        for pol in pols:
+            if pol != "-" and "=" in pol:
+                os.environ["RT_SPT_TUNE"] = pol + ("," + tune0 if tune0 else "")
+            elif pol != "-":
                 n1, hw = pol.split(":")
                 os.environ["RT_SPT_TUNE"] = "coop=%s,coop_waves=%s" % (n1, hw) + ("," + tune0 if tune0 else "")
+            else:
+                os.environ.pop("RT_SPT_TUNE", None) if tune0 is None else os.environ.__setitem__("RT_SPT_TUNE", tune0)
             out = bufs()
             res = []
             for k in range(N):
