@@ -136,30 +136,11 @@ __device__ __forceinline__ float sphere_cand(float4 g, const ray3 &r, int &res)
     return cand;
 }
 
-// plane_intersect, :95-109.
-__device__ __forceinline__ float plane_cand(float4 g, const ray3 &r)
-{
-    const float d = g.x * r.d.x + g.y * r.d.y + g.z * r.d.z;
-    float cand = __builtin_inff();
-    if (d != 0) {
-        const float t = -((g.x * r.o.x + g.y * r.o.y + g.z * r.o.z) + g.w) / d;
-        if (t > 0) cand = t;
-    }
-    return cand;
-}
-
-#ifndef RT_SPHERE_EXIT
-#define RT_SPHERE_EXIT 0      // occluder spheres: all-occluded exit after each sphere some lane may hit (A/B: 1; off measured faster)
-#endif
-#ifndef RT_PLANE_ONECHECK
-#define RT_PLANE_ONECHECK 1   // occluder planes: one all-occluded check before the loop, not per plane (A/B: 0)
-#endif
-#ifndef RT_Q_LEAN
-#define RT_Q_LEAN 3         // trace()'s loops without per-lane branches: bit 0 spheres, bit 1 planes (A/B: 0)
-#endif
-
-// plane_cand without branches: the division for every lane, its result kept
-// only where the reference divides (d != 0) and t > 0.
+// plane_intersect (:95-109) without branches: the division for every lane,
+// its result kept only where the reference divides (d != 0) and t > 0.  (The
+// per-lane-branch forms of this and of the sphere loops cost more exec-mask
+// instructions than VALU, and an all-occluded exit per occluder sphere or
+// per plane did not pay: profiles/r04.)
 __device__ __forceinline__ float plane_cand_lean(float4 g, const ray3 &r)
 {
     const float d = g.x * r.d.x + g.y * r.d.y + g.z * r.d.z;
@@ -177,69 +158,93 @@ __device__ __forceinline__ v3 normal_at(const Scene &S, int p, v3 pt)
     return mk(0.f, 0.f, 0.f);
 }
 
-// raytrace, :179-281.  EXACT: the specular factor by rtm::pow_d (else
-// spec20's certified shortcut, h.amb when it cannot certify).
+// raytrace's nearest hit (:181-193: below 1e7, lowest index on ties) for R
+// rays per lane in lock-step: each sphere and plane record read once for all
+// of them, their dependency chains interleaved (R = 2 in the latency-bound
+// root kernel).  sphere_cand as one wave-uniform branch over a straight-line
+// body (sqrt_nr for every lane, its range checked once per loop).  det <= 0
+// or NaN needs no test of its own: sqrt_nr returns NaN there (v_rsq of a
+// negative, 0 x inf at zero), so i2 > 0 fails.
+template <int R>
+__device__ __forceinline__ void nearest_n(const Scene &S, const ray3 (&ray)[R], float (&dist)[R], int (&prim)[R],
+                                          int (&result)[R])
+{
+    bool bad[R];
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+        dist[q] = 10000000.0f;
+        prim[q] = -1;
+        result[q] = 1;
+        bad[q] = false;
+    }
+    for (int k = 0; k < S.ns; k++) {
+        const float4 g = S.sph[k];
+        float b[R], det[R];
+        bool anyp = false;
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const float vx = ray[q].o.x - g.x, vy = ray[q].o.y - g.y, vz = ray[q].o.z - g.z;
+            b[q] = vx * ray[q].d.x + vy * ray[q].d.y + vz * ray[q].d.z;
+            b[q] = -b[q];
+            det[q] = (b[q] * b[q]) - (vx * vx + vy * vy + vz * vz) + g.w;
+            anyp = anyp || det[q] > 0;
+        }
+        if (wave_any(anyp)) {
+            const int id = S.sph_id[k];
+#pragma unroll
+            for (int q = 0; q < R; q++) {
+                const float sq = sqrt_nr(det[q]);
+                bad[q] = bad[q] || (det[q] > 0 && !sqrt_nr_ok(det[q]));
+                const float i1 = b[q] - sq, i2 = b[q] + sq;
+                const float c = i1 < 0 ? i2 : i1;
+                const bool take = i2 > 0 && (c < dist[q] || (c == dist[q] && prim[q] >= 0 && id < prim[q]));
+                dist[q] = take ? c : dist[q];
+                prim[q] = take ? id : prim[q];
+                result[q] = take ? (i1 < 0 ? -1 : 1) : result[q];
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+        if (wave_any(bad[q])) {                             // (rare: det outside sqrt_nr's range)
+            dist[q] = 10000000.0f;
+            prim[q] = -1;
+            result[q] = 1;
+            for (int k = 0; k < S.ns; k++) {
+                int res;
+                const float c = sphere_cand(S.sph[k], ray[q], res);
+                const int id = S.sph_id[k];
+                if (res && (c < dist[q] || (c == dist[q] && prim[q] >= 0 && id < prim[q]))) {
+                    dist[q] = c; prim[q] = id; result[q] = res;
+                }
+            }
+        }
+    }
+#pragma unroll 4
+    for (int k = 0; k < S.np; k++) {
+        const float4 g = S.pln[k];
+        const int id = S.pln_id[k];
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const float c = plane_cand_lean(g, ray[q]);
+            const bool take = c < dist[q] || (c == dist[q] && prim[q] >= 0 && id < prim[q]);
+            dist[q] = take ? c : dist[q];
+            prim[q] = take ? id : prim[q];
+            result[q] = take ? 1 : result[q];
+        }
+    }
+}
+
+// The rest of raytrace (:195-281) from the nearest hit.  EXACT: the specular
+// factor by rtm::pow_d (else spec20's certified shortcut, h.amb when it
+// cannot certify).
 template <bool COUNT, bool EXACT = false, bool UNCERT = false>
-__device__ Hit trace(const Scene &S, const ray3 &ray)
+__device__ Hit shade_hit(const Scene &S, const ray3 &ray, float dist, int prim, int result)
 {
     Hit h;
     h.amb = false;
     h.col = mk(0.f, 0.f, 0.f);
     h.pi = mk(0.f, 0.f, 0.f);
-    h.result = 1;
-    // :181-193 nearest hit below 1e7, lowest index on ties.
-    float dist = 10000000.0f;
-    int prim = -1, result = 1;
-    bool bad = !(RT_Q_LEAN & 1);
-    if (RT_Q_LEAN & 1) {
-        // sphere_cand as one wave-uniform branch over a straight-line body
-        // (sqrt_nr for every lane, its range checked once per loop): the
-        // nested per-lane branches cost more mask instructions than VALU.
-        // det <= 0 or NaN needs no test of its own: sqrt_nr returns NaN
-        // there (v_rsq of a negative, 0 x inf at zero), so i2 > 0 fails.
-        for (int k = 0; k < S.ns; k++) {
-            const float4 g = S.sph[k];
-            const float vx = ray.o.x - g.x, vy = ray.o.y - g.y, vz = ray.o.z - g.z;
-            float b = vx * ray.d.x + vy * ray.d.y + vz * ray.d.z;
-            b = -b;
-            const float det = (b * b) - (vx * vx + vy * vy + vz * vz) + g.w;
-            if (wave_any(det > 0)) {
-                const float sq = sqrt_nr(det);
-                bad = bad || (det > 0 && !sqrt_nr_ok(det));
-                const float i1 = b - sq, i2 = b + sq;
-                const float c = i1 < 0 ? i2 : i1;
-                const int id = S.sph_id[k];
-                const bool take = i2 > 0 && (c < dist || (c == dist && prim >= 0 && id < prim));
-                dist = take ? c : dist;
-                prim = take ? id : prim;
-                result = take ? (i1 < 0 ? -1 : 1) : result;
-            }
-        }
-    }
-    if (wave_any(bad)) {                                    // (rare: det outside sqrt_nr's range)
-        dist = 10000000.0f;
-        prim = -1;
-        result = 1;
-        for (int k = 0; k < S.ns; k++) {
-            int res;
-            const float c = sphere_cand(S.sph[k], ray, res);
-            const int id = S.sph_id[k];
-            if (res && (c < dist || (c == dist && prim >= 0 && id < prim))) { dist = c; prim = id; result = res; }
-        }
-    }
-#pragma unroll 4
-    for (int k = 0; k < S.np; k++) {
-        const float c = (RT_Q_LEAN & 2) ? plane_cand_lean(S.pln[k], ray) : plane_cand(S.pln[k], ray);
-        const int id = S.pln_id[k];
-        if (RT_Q_LEAN & 2) {
-            const bool take = c < dist || (c == dist && prim >= 0 && id < prim);
-            dist = take ? c : dist;
-            prim = take ? id : prim;
-            result = take ? 1 : result;
-        } else if (c < dist || (c == dist && prim >= 0 && id < prim)) {
-            dist = c; prim = id; result = 1;
-        }
-    }
     h.prim = prim;
     h.result = result;
     h.dist = dist;
@@ -282,23 +287,20 @@ __device__ Hit trace(const Scene &S, const ray3 &ray)
                 // the point; the reference stops at the first, so only its
                 // position matters (test counter).
                 int first = 0x7fffffff;
-                bool sbad = !(RT_Q_LEAN & 1);
-                if (RT_Q_LEAN & 1) {
-                    for (int k = 0; k < S.nos; k++) {
-                        const float4 g = S.osph[k];
-                        const float vx = r.o.x - g.x, vy = r.o.y - g.y, vz = r.o.z - g.z;
-                        float b = vx * r.d.x + vy * r.d.y + vz * r.d.z;
-                        b = -b;
-                        const float det = (b * b) - (vx * vx + vy * vy + vz * vz) + g.w;
-                        if (wave_any(det > 0)) {
-                            const float sq = sqrt_nr(det);
-                            sbad = sbad || (det > 0 && !sqrt_nr_ok(det));
-                            const float i1 = b - sq, i2 = b + sq;
-                            const float c = i1 < 0 ? i2 : i1;
-                            const bool occ = i2 > 0 && c < len;
-                            first = occ ? min(first, S.osph_pos[k]) : first;
-                            if (!COUNT && RT_SPHERE_EXIT && !wave_any(first == 0x7fffffff)) break;
-                        }
+                bool sbad = false;
+                for (int k = 0; k < S.nos; k++) {
+                    const float4 g = S.osph[k];
+                    const float vx = r.o.x - g.x, vy = r.o.y - g.y, vz = r.o.z - g.z;
+                    float b = vx * r.d.x + vy * r.d.y + vz * r.d.z;
+                    b = -b;
+                    const float det = (b * b) - (vx * vx + vy * vy + vz * vz) + g.w;
+                    if (wave_any(det > 0)) {
+                        const float sq = sqrt_nr(det);
+                        sbad = sbad || (det > 0 && !sqrt_nr_ok(det));
+                        const float i1 = b - sq, i2 = b + sq;
+                        const float c = i1 < 0 ? i2 : i1;
+                        const bool occ = i2 > 0 && c < len;
+                        first = occ ? min(first, S.osph_pos[k]) : first;
                     }
                 }
                 if (wave_any(sbad)) {
@@ -313,10 +315,8 @@ __device__ Hit trace(const Scene &S, const ray3 &ray)
                 const bool pl_any = COUNT || wave_any(first == 0x7fffffff);   // (all occluded by a sphere: no plane test)
 #pragma unroll 4
                 for (int k = 0; pl_any && k < S.nop; k++) {
-                    if (!COUNT && !RT_PLANE_ONECHECK && !wave_any(first == 0x7fffffff)) break;
-                    const float c = (RT_Q_LEAN & 2) ? plane_cand_lean(S.opln[k], r) : plane_cand(S.opln[k], r);
-                    if (RT_Q_LEAN & 2) first = c < len ? min(first, S.opln_pos[k]) : first;
-                    else if (c < len) first = min(first, S.opln_pos[k]);
+                    const float c = plane_cand_lean(S.opln[k], r);
+                    first = c < len ? min(first, S.opln_pos[k]) : first;
                 }
                 if (first != 0x7fffffff) shade = 0.0f;
                 tests += first != 0x7fffffff ? (unsigned)first + 1u : (unsigned)S.nnonlight;
@@ -348,6 +348,17 @@ __device__ Hit trace(const Scene &S, const ray3 &ray)
     }
     h.cnt = COUNT ? (tests | (shadows << 16)) : 0u;
     return h;
+}
+
+// raytrace, :179-281.
+template <bool COUNT, bool EXACT = false, bool UNCERT = false>
+__device__ Hit trace(const Scene &S, const ray3 &ray)
+{
+    const ray3 rr[1] = {ray};
+    float dist[1];
+    int prim[1], result[1];
+    nearest_n<1>(S, rr, dist, prim, result);
+    return shade_hit<COUNT, EXACT, UNCERT>(S, ray, dist[0], prim[0], result[0]);
 }
 
 // The term the pixel's accumulator receives when `n` is popped (:351-368).
@@ -686,15 +697,38 @@ root_kernel(QArgs A, int row_end, float DX, float DY, unsigned long long *__rest
     // While the pixel's trees have no children their terms are final: they
     // are summed here in the reference's order; the trees from the first one
     // with children (or with an uncertified term) on are recorded.
+    // Two sub-samples' nearest hits are found together (nearest_n<2>: each
+    // primitive record read once for both, two dependency chains per lane),
+    // then each is shaded, summed or recorded and queued in sub-sample order
+    // (1080p -2 %, 800 x 600 level; at 7 or 6 waves per SIMD instead of 8,
+    // without the 12-B spill: slower; profiles/r06/queue_root_rays_ab.log).
     float ax = 0.f, ay = 0.f, az = 0.f;
     int kfirst = NSUB;
-    for (int sub = 0; sub < NSUB; sub++) {
+#pragma unroll 1
+    for (int s0 = 0; s0 < NSUB; s0 += 2) {
+        const int s1 = min(s0 + 1, NSUB - 1);
+        const ray3 rr[2] = {primary(s0, x, y, DX, DY).r, primary(s1, x, y, DX, DY).r};
+        float dd[2];
+        int pp[2], rs[2];
+        if (s0 + 1 < NSUB) {
+            nearest_n<2>(S, rr, dd, pp, rs);
+        } else {
+            const ray3 r1[1] = {rr[0]};
+            float d1[1];
+            int p1[1], q1[1];
+            nearest_n<1>(S, r1, d1, p1, q1);
+            dd[0] = d1[0]; pp[0] = p1[0]; rs[0] = q1[0];
+        }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const int sub = s0 + j;
+        if (sub >= NSUB) break;
         Node n;
         Hit h;
         int f = 0;
         if (active) {
             n = primary(sub, x, y, DX, DY);
-            h = trace<COUNT, false, UNCERT>(S, n.r);
+            h = shade_hit<COUNT, false, UNCERT>(S, n.r, dd[j], pp[j], rs[j]);
             f = child_flags(S, n, h);
         }
         const int tree = sub * A.npix + pix;
@@ -714,6 +748,7 @@ root_kernel(QArgs A, int row_end, float DX, float DY, unsigned long long *__rest
                 if (h.amb) flag_tree(A, tree);
             }
         }
+    }
     }
     if (active) A.psum[pix] = make_float4(ax, ay, az, __int_as_float(kfirst));
     if (COUNT) flush_counters<4>(counters, cnt);
@@ -775,9 +810,6 @@ level_kernel(QArgs A, int L)
 #define RT_Q_FOLD 8         // records per batch of the fold's breadth-first walk (A/B: 2,4,6,8,12,16 -> 8 best)
 #endif
 constexpr int FOLD = RT_Q_FOLD;
-#ifndef RT_Q_FOLD_ROOTS
-#define RT_Q_FOLD_ROOTS 9   // final_kernel: trees whose root records are read together (all nine; A/B: 1, 3, 5)
-#endif
 
 template <bool COUNT, int COLS>
 __device__ __forceinline__ void fold_tree_from(const QArgs &A, float4 c0, int2 ch, int (*ring)[COLS], float &ax,
@@ -857,27 +889,21 @@ final_kernel(QArgs A, int row_end, uint32_t *__restrict__ out, unsigned long lon
     if (x < A.w && y < row_end && !pix_flagged(A, pix)) {
         const float4 ps = A.psum[pix];
         float ax = ps.x, ay = ps.y, az = ps.z;
-#if RT_Q_FOLD_ROOTS > 1
-        // The root records of RT_Q_FOLD_ROOTS trees loaded together (one
-        // latency instead of one per tree), then each tree folded in order.
-        constexpr int T = RT_Q_FOLD_ROOTS;
-        for (int s0 = __float_as_int(ps.w); s0 < NSUB; s0 += T) {
-            float4 c0[T];
-            int2 ch[T];
+        // The remaining trees' root records loaded together (one latency
+        // instead of one per tree; reading fewer at a time, 1 / 3 / 5, was
+        // slower), then each tree folded in order.
+        const int s0 = __float_as_int(ps.w);
+        float4 c0[NSUB];
+        int2 ch[NSUB];
 #pragma unroll
-            for (int j = 0; j < T; j++) {
-                const int tree = (s0 + j < NSUB ? s0 + j : s0) * A.npix + pix;
-                c0[j] = A.rcol[tree];
-                ch[j] = A.rchild[tree];
-            }
-#pragma unroll
-            for (int j = 0; j < T; j++)
-                if (s0 + j < NSUB) fold_tree_from<COUNT, 256>(A, c0[j], ch[j], ring, ax, ay, az, cnt);
+        for (int j = 0; j < NSUB; j++) {
+            const int tree = (j >= s0 ? j : NSUB - 1) * A.npix + pix;   // (s0 = NSUB: nothing left)
+            c0[j] = A.rcol[tree];
+            ch[j] = A.rchild[tree];
         }
-#else
-        for (int sub = __float_as_int(ps.w); sub < NSUB; sub++)
-            fold_tree<COUNT, 256>(A, sub * A.npix + pix, ring, ax, ay, az, cnt);
-#endif
+#pragma unroll
+        for (int j = 0; j < NSUB; j++)
+            if (j >= s0) fold_tree_from<COUNT, 256>(A, c0[j], ch[j], ring, ax, ay, az, cnt);
         out[(size_t)y * A.w + x] = pack_pixel(ax, ay, az);
     }
     if (COUNT) flush_counters<4>(counters, cnt);

@@ -127,6 +127,13 @@ int state(DeviceState **out)
         }
         memset(st->pool_ovf, 0, POOL_FITS * sizeof(int));
         g_states[dev] = st;
+        // The second stream (two-slab level-pass frames) is created with the
+        // state, not at its first use: created mid-run it ran the 1080p
+        // queue frame's second slab measurably less concurrently (1.43-1.45
+        // -> 1.36-1.40 ms; Whitted 1080p best 1.49-1.50 -> 1.47-1.48 ms,
+        // profiles/r06/aux_stream_at_state_ab.log).  Not fatal here: a later
+        // aux_stream() call retries and reports.
+        (void)aux_stream(*st);
     } else {
         hipError_t e = hipSetDevice(dev);
         if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
