@@ -1275,9 +1275,6 @@ int resident_blocks(K kernel)
     return cus * per;
 }
 
-#ifndef RT_WH_TIR_BLOCKS
-#define RT_WH_TIR_BLOCKS 64
-#endif
 template <bool COUNT>
 int launch_wavefront(const rt::whitted::WfArgs &A, int w, int rows, int row_end, const float *d_sx,
                      const float *d_sy, float DX, float DY, unsigned long long *cnt, hipStream_t s, uint32_t *d_xrgb)
@@ -1288,7 +1285,7 @@ int launch_wavefront(const rt::whitted::WfArgs &A, int w, int rows, int row_end,
     const int qblocks = (int)std::min<long long>(((long long)A.pool + 255) / 256, 2048);
     hipLaunchKernelGGL(root_kernel<COUNT>, tiles, block, 0, s, A, row_end, d_sx, d_sy, DX, DY, cnt);
     for (int L = 1; L < LEVELS; L++) {
-        hipLaunchKernelGGL(tir_kernel, dim3(RT_WH_TIR_BLOCKS), dim3(64), 0, s, A, L - 1, d_sx, d_sy, DX, DY);
+        hipLaunchKernelGGL(tir_kernel, dim3(64), dim3(64), 0, s, A, L - 1, d_sx, d_sy, DX, DY);   // (256 / 1024 blocks: level)
         hipLaunchKernelGGL(level_kernel<COUNT>, dim3(level_blocks), block, 0, s, A, L, cnt);
     }
     hipLaunchKernelGGL(fixup_kernel<COUNT>, dim3(256), dim3(64), 0, s, A, d_sx, d_sy, DX, DY, cnt);
