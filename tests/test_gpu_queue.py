@@ -178,10 +178,11 @@ def test_bad_arguments(rt):
 
 
 def test_sphere_loop_exact_redo(rt):
-    """The queue tracer's lean sphere loops (queue.hip RT_Q_LEAN) redo a loop
-    exactly when a discriminant leaves sqrt_nr's range: a sphere of infinite
-    radius (never hit) forces that redo in every loop; frame and counters stay
-    the oracle's."""
+    """The queue tracer's lean sphere loops (queue.hip nearest_n, the shadow
+    loop of shade_hit) redo a loop exactly when a discriminant leaves sqrt_nr's
+    range: a sphere of infinite radius (never hit) forces that redo in every
+    loop, for the root pass's two-ray form too; frame and counters stay the
+    oracle's."""
     P, n = O.queue_scene()
     p = P[n]
     p.type = 1
