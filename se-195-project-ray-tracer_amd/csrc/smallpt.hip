@@ -2219,14 +2219,15 @@ size_t wide_lds_bytes(int wnodes, int wdepth, int wpb, bool counted = true)
 //   routed=N    tier-2 tiles routed one per SIMD (default 4 x blocks when
 //               there is no cooperative tier, else 0)
 //   walk=B/P/S  wide_walk: trip budget per call, leaf batch threshold and
-//               early stop, both in 1/64 of the call's lanes (16/16/32)
+//               early stop, both in 1/64 of the call's lanes (16/16/32; the
+//               stop 16 in windows with a cooperative tier)
 //   prio=A/B/C  priority-levelling boundaries in 1/256 of the samples
 //               (64/128/192 for the 4-wave block shape, 128/192/224 for 16)
 //   wpb=4|16    full-scan block shape (default: by waves of work per SIMD)
 //   blocks=N    8-wide persistent grid size (default: one block per CU)
 struct SptTune {
     int coop = -1, coop_g = 0, coop_waves = -1, routed = -1;
-    int budget = 16, batch = 16, stop = 32;
+    int budget = 16, batch = 16, stop = -1;     // (stop -1: by window, see launch)
     int prio[3] = {-1, -1, -1};
     int wpb = 0, blocks = 0;
 };
@@ -2397,8 +2398,14 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
     const int nheavy = std::min(n1, 0xffff) | (std::min(n2, 0xffff) << 16);
     int split = 0;
     if (GEO == rt::smallpt::GEO_WIDE) {
+        // A walk call returns once <= stop/64 of the lanes that started it
+        // still walk: 32 on the full frame; 16 in a window with a cooperative
+        // tier, where the heaviest waves' chains bound the share (round 6,
+        // with the deferred leaf sections: N = 8 9.5 -> 9.2 ms, N = 4 13.2 ->
+        // 12.8 ms, profiles/r06/c4_walk_stop_sweep.log).
+        const int stop = tu.stop >= 0 ? tu.stop : (n1 > 0 ? 16 : 32);
         split = sp | (std::min(std::max(tu.budget, 1), 255) << 8) | (std::min(std::max(tu.batch, 0), 64) << 16) |
-                (std::min(std::max(tu.stop, 0), 64) << 24);
+                (std::min(std::max(stop, 0), 64) << 24);
     }
     // (the kernel carries the cooperative walk only when this launch has a
     // cooperative tier, and only the group size it uses)
