@@ -3,7 +3,8 @@
 per tuning, warm frames (the first records the tile costs, the learnt order
 applies from the next), then REPS timed frames (HIP events, median and min),
 each frame checked against the reference-core golden hashes.  GROUP=k/N
-times an interleaved share instead of the full frame.
+times an interleaved share instead of the full frame; COUNTED=1 times the
+full-counter kernels (all four reference counters).
 
     TUNES="-;coop=512;walk=8/16/32" REPS=5 python tools/tune_ab.py   ("-": the defaults)
 """
@@ -23,6 +24,7 @@ W, H, SPP = int(os.environ.get("W", 1920)), int(os.environ.get("H", 1080)), int(
 REPS, WARM = int(os.environ.get("REPS", 5)), int(os.environ.get("WARM", 3))
 TUNES = os.environ.get("TUNES", "-").split(";")
 GROUP = os.environ.get("GROUP")
+COUNTED = os.environ.get("COUNTED") == "1"
 dev = torch.device("cuda", 0)
 spheres, n, cam = rtamd.scenes.complex10k()
 rtamd.scenes.update_camera(cam, W, H)
@@ -40,16 +42,18 @@ for tune in TUNES:
     seeds = torch.empty_like(seeds0)
     col = torch.zeros(3 * W * H, dtype=torch.float32, device=dev)
     px = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+    cptr = C.cast(C.c_void_p(cnt.data_ptr()), C.POINTER(C.c_uint64)) if COUNTED else None
 
     def run():
         if GROUP:
             k, N = (int(v) for v in GROUP.split("/"))
             rtamd.check(L.spt_scene_render_groups_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
-                                                        seeds.data_ptr(), px.data_ptr(), W, H, k, N, 0, SPP, 0, None,
+                                                        seeds.data_ptr(), px.data_ptr(), W, H, k, N, 0, SPP, 0, cptr,
                                                         st.cuda_stream))
         else:
             rtamd.check(L.spt_scene_render_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
-                                                 seeds.data_ptr(), px.data_ptr(), W, H, 0, H, 0, SPP, 0, None,
+                                                 seeds.data_ptr(), px.data_ptr(), W, H, 0, H, 0, SPP, 0, cptr,
                                                  st.cuda_stream))
 
     for _ in range(WARM):
