@@ -788,7 +788,7 @@ __device__ __forceinline__ float grp_min(float v)
     constexpr int ID = 0x7fffffff;
     int i = __float_as_int(v);
     i = min(i, __builtin_amdgcn_update_dpp(ID, i, 0xB1, 0xF, 0xF, false));
-    i = min(i, __builtin_amdgcn_update_dpp(ID, i, 0x4E, 0xF, 0xF, false));
+    if (G >= 4) i = min(i, __builtin_amdgcn_update_dpp(ID, i, 0x4E, 0xF, 0xF, false));
     if (G == 8) i = min(i, __builtin_amdgcn_update_dpp(ID, i, 0x141, 0xF, 0xF, false));
     return __int_as_float(i);
 }
@@ -797,7 +797,7 @@ __device__ __forceinline__ int grp_max(int v)
 {
     constexpr int ID = (int)0x80000000;
     v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0xB1, 0xF, 0xF, false));
-    v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0x4E, 0xF, 0xF, false));
+    if (G >= 4) v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0x4E, 0xF, 0xF, false));
     if (G == 8) v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0x141, 0xF, 0xF, false));
     return v;
 }
@@ -1021,10 +1021,11 @@ __device__ __forceinline__ bool coop_leaves(const BvhView &B, const ray3 &r, boo
                                             const unsigned *Lw, int oct, int n1, unsigned l1, int n2, unsigned l2,
                                             int pos, int gbase, float &t, int &bpos, int &id)
 {
+    constexpr int NL = G == 2 ? 1 : RT_SPT_COOP_NL;   // (two lanes: four spheres a lane per leaf already)
     while (l1 | l2) {
-        int fa[RT_SPT_COOP_NL], ca[RT_SPT_COOP_NL];
+        int fa[NL], ca[NL];
 #pragma unroll
-        for (int q = 0; q < RT_SPT_COOP_NL; q++) {
+        for (int q = 0; q < NL; q++) {
             fa[q] = ca[q] = 0;
             if (l1 | l2) {
                 const bool first = l1 != 0;
@@ -1037,7 +1038,7 @@ __device__ __forceinline__ bool coop_leaves(const BvhView &B, const ray3 &r, boo
                 ca[q] = wq >> 24;
             }
         }
-        if (leaf_coop<COUNT, G, RT_SPT_COOP_NL, LOC>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id))
+        if (leaf_coop<COUNT, G, NL, LOC>(B, r, shadow, maxt, fa, ca, pos, gbase, t, bpos, id))
             return true;
     }
     return false;
@@ -1390,7 +1391,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
     const int grp = group_order ? (slot < nslots ? group_order[slot] : -1) : slot;
     const bool gvalid = (unsigned)grp < (unsigned)((ntiles + 3) >> 2);
     const int tile = grp * 4 + (item & 3);
-    const int li = coop ? (sub << (6 - hs)) + (cg == 8 ? lane >> 3 : lane >> 2) : lane;   // pixel of the 8x8 tile
+    const int li = coop ? (sub << (6 - hs)) + (lane >> hs) : lane;   // pixel of the 8x8 tile
     const bool lead = !coop || (lane & (cg - 1)) == 0;  // the lane that stores the pixel and counts
     unsigned long long t_start = 0;
     if (SCHED) t_start = __builtin_amdgcn_s_memrealtime();
@@ -1685,7 +1686,7 @@ render_kernel(const rt_sphere *__restrict__ spheres, int nspheres, rt_camera cam
 #endif
                 if (!walking) wide_begin<COUNT>(bvh, ray, shadow, t, walk);
                 if constexpr (CG != 0)
-                    walking = coop ? !wide_walk_coop<COUNT, (CG == 4 ? 4 : 8)>(bvh, wL, wstk, ray, shadow, walk, split)
+                    walking = coop ? !wide_walk_coop<COUNT, (CG ? CG : 8)>(bvh, wL, wstk, ray, shadow, walk, split)
                                    : !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
                 else
                     walking = !wide_walk<COUNT>(bvh, wL, wstk, ray, shadow, walk, split);
@@ -2213,8 +2214,8 @@ size_t wide_lds_bytes(int wnodes, int wdepth, int wpb, bool counted = true)
 //   coop=N      cooperative (tier-1) tiles of an ordered 8-wide launch
 //               (default: 2 x CUs at <= 5 waves of work per SIMD, 4 x CUs at
 //               <= 10, else 0)
-//   coop_g=G    lanes per pixel of those tiles, 8 or 4 (default 8 at <= 5
-//               waves per SIMD, 4 above)
+//   coop_g=G    lanes per pixel of those tiles, 8, 4 or 2 (default 8 at <= 5
+//               waves of work per SIMD, 4 at <= 10, 2 at <= 20)
 //   coop_waves=K waves of each block that fetch tier-1 sub-items first (16)
 //   routed=N    tier-2 tiles routed one per SIMD (default 4 x blocks when
 //               there is no cooperative tier, else 0)
@@ -2248,7 +2249,7 @@ SptTune spt_tune()
         const std::string k = kv.substr(0, eq);
         const char *v = kv.c_str() + eq + 1;
         if (k == "coop") t.coop = std::max(atoi(v), 0);
-        else if (k == "coop_g") t.coop_g = atoi(v) == 4 ? 4 : 8;
+        else if (k == "coop_g") t.coop_g = atoi(v) == 4 ? 4 : (atoi(v) == 2 ? 2 : 8);
         else if (k == "coop_waves") t.coop_waves = std::min(std::max(atoi(v), 0), 16);
         else if (k == "routed") t.routed = std::max(atoi(v), 0);
         else if (k == "walk") sscanf(v, "%d/%d/%d", &t.budget, &t.batch, &t.stop);
@@ -2362,7 +2363,8 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
     // many waves of work per SIMD (a full frame: 31.6) is throughput-bound:
     // routing only.  A window of few (a multi-GPU rank's share: N = 8 is 4.0,
     // N = 4 7.9, N = 2 15.8) is bound by its heaviest tiles' sample chains,
-    // which the cooperative walk shortens ~2x at ~3x their issue cost.
+    // which the cooperative walk shortens ~2x at ~3x their issue cost (8
+    // lanes per pixel at N = 8, 4 at N = 4, 2 at N = 2).
     // configs[4], 64 spp (profiles/r03/c4_coop_*.log): N = 8 windows
     // 18.0-19.8 -> 11.4-15.1 ms, N = 4 18.7 -> 17 ms; see DESIGN.md.
     const SptTune &tu = g.tune;
@@ -2384,6 +2386,15 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
             n1 = 4 * sc.cus;
             hw = 16;
             cg = 4;
+        } else if (wps <= 20.0) {
+            // An N = 2 share (15.8 waves of work per SIMD): still bound by its
+            // heaviest chains, and too full for four- or eight-lane tiers to
+            // pay (20.5 -> 19.8-23 ms); two lanes per pixel for the heaviest
+            // 1,024 tiles halve their walks at the least duplicated shading:
+            // 20.5 -> 19.3-19.5 ms (round 6, c4_coop_g2_ab.log; 768-1,024
+            // best, 1,280+ slower; at N = 4 two lanes lose to four).
+            n1 = 4 * sc.cus;
+            cg = 2;
         }
         if (tu.coop_g) cg = tu.coop_g;
         if (tu.coop >= 0) n1 = tu.coop;
@@ -2392,7 +2403,7 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
         if (tu.routed >= 0) n2 = tu.routed;
         n1 = std::min(n1, 4 * g.nslots);
         n2 = std::min(n2, 4 * g.nslots - n1);
-        if (n1 > 0) sp = (cg == 8 ? 3 : 2) | 4 | (hw << 3);
+        if (n1 > 0) sp = (cg == 8 ? 3 : cg == 4 ? 2 : 1) | 4 | (hw << 3);
         kcg = n1 > 0 ? cg : 0;
     }
     const int nheavy = std::min(n1, 0xffff) | (std::min(n2, 0xffff) << 16);
@@ -2413,6 +2424,7 @@ int launch(const Shape &g, hipStream_t s, const spt_scene &sc, const rt_camera &
     if constexpr (GEO == rt::smallpt::GEO_WIDE) {
         if (kcg == 8) kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 8>;
         else if (kcg == 4) kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 4>;
+        else if (kcg == 2) kern = rt::smallpt::render_kernel<DL, COUNT, GEO, DUAL, RAYS, 2>;
     }
     hipLaunchKernelGGL(kern, dim3(g.nblocks), dim3(64 * g.wpb), lds, s,
                        sc.d_spheres, n, cam, colors, sin, sout, pixels, w, h, r0, r1, g.tiles_x, g.ntiles, g.nslots, g.gstride, first,

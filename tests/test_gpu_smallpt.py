@@ -180,20 +180,20 @@ def test_configs4_full_size_golden(rt, oracle, counted, walk, monkeypatch):
             assert f.counters[3] == w * h * 64
 
 
-@pytest.mark.parametrize("coop", ["512", "4096"])
+@pytest.mark.parametrize("tune", ["coop=512", "coop=4096", "coop=1024,coop_g=4", "coop=1024,coop_g=2"])
 @pytest.mark.parametrize("counted", [False, True])
-def test_configs4_cooperative_walk_golden(rt, oracle, counted, coop, monkeypatch):
-    """The heaviest tiles walk the 8-wide hierarchy eight lanes per pixel
-    (wide_walk_coop) once a learnt order exists: the 1st frame of a key
-    records the tile costs, the next ones dispatch the heaviest tiles
+def test_configs4_cooperative_walk_golden(rt, oracle, counted, tune, monkeypatch):
+    """The heaviest tiles walk the 8-wide hierarchy eight, four or two lanes
+    per pixel (wide_walk_coop<G>) once a learnt order exists: the 1st frame
+    of a key records the tile costs, the next ones dispatch the heaviest tiles
     cooperatively (forced here on the full frame, which by default only
-    routes them, with 512 and 4096 cooperative tiles beside 1024 routed
-    ones).  Every frame must equal the reference core's golden hashes
-    (configs[4], 1920x1080, 64 spp), counted (and the counters exact) and
-    uncounted."""
+    routes them: 512 and 4096 eight-lane tiles, 1024 four-lane and 1024
+    two-lane ones).  Every frame must equal the reference core's golden
+    hashes (configs[4], 1920x1080, 64 spp), counted (and the counters exact)
+    and uncounted."""
     import json
     import os
-    monkeypatch.setenv("RT_SPT_TUNE", "coop=" + coop)
+    monkeypatch.setenv("RT_SPT_TUNE", tune)
     gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
     g = gold["smallpt"]["1920x1080_64spp_complex10k"]
     spheres, n, cam = rt.scenes.complex10k()
