@@ -214,6 +214,46 @@ def test_configs4_cooperative_walk_golden(rt, oracle, counted, tune, monkeypatch
             assert list(f.counters) == first
 
 
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_configs4_rank_shares_golden(rt, oracle, nranks):
+    """BASELINE configs[4] split as the multi-GPU bench splits it: every
+    nranks-th 8-row group per rank (spt_scene_render_groups_async), each
+    share with a scene of its own that learns its order in a first frame, so
+    the later frames use the window class's default cooperative tier (two
+    lanes per pixel at N = 2, four at N = 4, eight at N = 8).  The assembled
+    frame of the third round equals the reference core's golden hashes."""
+    import ctypes as C
+    import json
+    import os
+    import torch
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
+    g = gold["smallpt"]["1920x1080_64spp_complex10k"]
+    spheres, n, cam = rt.scenes.complex10k()
+    w, h = 1920, 1080
+    rt.scenes.update_camera(cam, w, h)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    L = rt.lib()
+    seeds0 = torch.from_numpy(rt.scenes.seeds(w, h).view(np.int32)).to(dev)
+    scenes = [rt.SmallptScene(spheres, n) for _ in range(nranks)]
+    try:
+        for _ in range(3):                     # learn, then the learnt order and its tiers
+            col = torch.zeros(3 * w * h, dtype=torch.float32, device=dev)
+            seeds = torch.zeros_like(seeds0)
+            px = torch.zeros(w * h, dtype=torch.int32, device=dev)
+            for k, sc in enumerate(scenes):
+                rt.check(L.spt_scene_render_groups_async(sc.handle, C.byref(cam), col.data_ptr(), seeds0.data_ptr(),
+                                                         seeds.data_ptr(), px.data_ptr(), w, h, k, nranks, 0, 64, 0,
+                                                         None, st))
+            torch.cuda.synchronize()
+        got = (oracle.fnv1a64(col.cpu().numpy()), oracle.fnv1a64(px.cpu().numpy().view(np.uint32)),
+               oracle.fnv1a64(seeds.cpu().numpy().view(np.uint32)))
+        assert got == (g["colors"], g["pixels"], g["seeds"])
+    finally:
+        for sc in scenes:
+            sc.close()
+
+
 def test_async_device_paths(rt, oracle):
     """spt_scene_render_async and spt_render_async on device buffers, rows
     split in two calls, seeds_in != seeds_out."""
