@@ -7,6 +7,7 @@ compared bit for bit (colours, seeds, pixels, work counters).
 
     N=60 python tools/bvh_stress.py
     REPEAT=3 N=60 python tools/bvh_stress.py   # learnt order: cooperative heavy tiles (small frames)
+    RT_SPT_TUNE=coop_g=2 REPEAT=2 N=60 python tools/bvh_stress.py   # ... at two (or 4) lanes per pixel
 """
 import os
 import sys
